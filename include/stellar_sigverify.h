@@ -1,0 +1,126 @@
+/*
+ * stellar_sigverify.h — C-ABI of the MI355X (gfx950) batched ed25519
+ * signature-verification engine for stellar-core.
+ *
+ * Drop-in boundary.  stellar-core verifies every ed25519 signature through one
+ * synchronous function:
+ *
+ *   bool stellar::PubKeyUtils::verifySig(PublicKey const&, Signature const&,
+ *                                        ByteSlice const&)
+ *     declared  /root/reference/src/crypto/SecretKey.h:139-140
+ *     defined   /root/reference/src/crypto/SecretKey.cpp:435-468
+ *
+ * which, on a verify-cache miss, calls libsodium
+ *   crypto_sign_verify_detached(sig, msg, msg_len, pk)   (SecretKey.cpp:461-463)
+ *
+ * The entry points below replace that libsodium call for WHOLE BATCHES of
+ * cache misses.  Verdicts are bit-identical to libsodium 1.0.18
+ * crypto_sign_verify_detached (cofactorless, S < L, small-order R/A and
+ * non-canonical A rejected) on every input.  The size-64 rule of
+ * SecretKey.cpp:441-444 is the caller's job (a Signature is an XDR opaque<64>;
+ * anything shorter never reaches this API), as is the verify cache
+ * (SecretKey.cpp:446-457,464-466) — see the C++ host mirror
+ * stellar-core_amd/csrc/host/PubKeyUtils.{h,cpp}.
+ *
+ * Conventions: plain pointers and sizes, caller-owned memory, no exceptions
+ * cross the boundary, every call returns SV_OK (0) or a negative SV_ERR_*.
+ * An error is NEVER a reject: on error the verdict buffer content is
+ * unspecified and the caller must treat the whole batch as unverified.
+ * All entry points are thread-safe; calls that target one device are
+ * serialised on that device's internal stream (its per-lane table workspace).
+ */
+#ifndef STELLAR_SIGVERIFY_H
+#define STELLAR_SIGVERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SV_OK 0
+#define SV_ERR_INVALID_ARG (-1)
+#define SV_ERR_NO_DEVICE (-2)
+#define SV_ERR_HIP (-3)
+#define SV_ERR_ALLOC (-4)
+#define SV_ERR_NOT_INIT (-5)
+#define SV_ERR_ALIGN (-6)
+
+/* Batch options.  A NULL opts pointer means "all defaults". */
+typedef struct sv_opts {
+  uint32_t struct_size; /* sizeof(sv_opts), for forward compatibility */
+  int32_t device;       /* -1 (default): shard contiguous slices over all devices; k >= 0: device k only */
+  uint32_t max_devices; /* 0 (default): no limit; else use at most this many devices when device == -1 */
+  uint32_t flags;       /* reserved, must be 0 */
+} sv_opts;
+
+/* Initialise every visible device (B-table, workspace, streams).  Idempotent.
+ * Called implicitly by the verify entry points. */
+int sv_init(void);
+/* Release all device resources.  Safe to call more than once. */
+void sv_shutdown(void);
+/* Number of usable devices (initialises on first use); negative on error. */
+int sv_device_count(void);
+/* Thread-local description of the last error on the calling thread. */
+const char* sv_last_error_string(void);
+const char* sv_version(void);
+
+/*
+ * Variable-length batch, host buffers (replaces n calls of
+ * crypto_sign_verify_detached made by PubKeyUtils::verifySig, SecretKey.cpp:461-463).
+ *   pk       n x 32 bytes   (PublicKey ed25519, uint256)
+ *   sig      n x 64 bytes   (R || S)
+ *   msg      message bytes; message i = msg[msg_off[i] .. msg_off[i] + msg_len[i])
+ *   verdict  n bytes out, 1 = valid, 0 = invalid
+ */
+int sv_ed25519_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                            const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
+                            uint8_t* verdict, const sv_opts* opts);
+
+/*
+ * Fixed-length batch, host buffers: message i = msg[i*msg_len .. (i+1)*msg_len).
+ * msg_len == 32 (transaction contents hashes, TransactionFrame.cpp:90-117)
+ * takes the single-SHA-512-block fast path.
+ */
+int sv_ed25519_verify_batch_fixed(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                                  uint32_t msg_len, size_t n, uint8_t* verdict, const sv_opts* opts);
+
+/*
+ * Device-resident batch on one device: every pointer is device memory on
+ * `device` (16-byte aligned pk/sig; for fixed_msg_len == 32 also msg).
+ * If fixed_msg_len != 0, message i = d_msg[i*fixed_msg_len ..] and
+ * d_msg_off/d_msg_len are ignored (may be NULL).  d_bitmap (optional, may be
+ * NULL) receives one bit per signature, 64 per word, bit (i % 64) of word
+ * i / 64 (wave-level ballot compaction of the verdicts).
+ * `stream` is a hipStream_t (NULL = legacy default stream): the work is
+ * ordered after prior work on `stream` and later work on `stream` is ordered
+ * after it; the call itself does not block.
+ */
+int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, const void* d_msg,
+                             const uint64_t* d_msg_off, const uint32_t* d_msg_len,
+                             uint32_t fixed_msg_len, size_t n, void* d_verdict, void* d_bitmap,
+                             void* stream);
+
+/*
+ * Synthetic-workload generator (device-resident): for i in [0, n) derive the
+ * keypair from seed i (RFC 8032, == crypto_sign_seed_keypair) and sign the
+ * 32-byte message i (== crypto_sign_detached).  Used by the bench to build
+ * the 1M..64M-signature datasets on the GPU box; its output is checked
+ * against libsodium-generated digests (tests/golden/digests.json).
+ */
+int sv_ed25519_sign_device(int device, const void* d_seed, const void* d_msg32, size_t n, void* d_pk,
+                           void* d_sig, void* stream);
+
+/* Kernel-time accounting for profiling: when enabled, every verify launch is
+ * bracketed by HIP events on the device's internal stream and the elapsed
+ * times are accumulated (read back with sv_kernel_time). */
+int sv_timing_enable(int enable);
+int sv_kernel_time(int device, double* total_ms, uint64_t* launches, uint64_t* signatures);
+int sv_kernel_time_reset(void);
+int sv_device_synchronize(int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STELLAR_SIGVERIFY_H */

@@ -1,0 +1,211 @@
+"""Python host binding of the MI355X ed25519 verification engine (stellar-core_amd).
+
+The product is the C-ABI library ``libstellar_sigverify.so`` built in-tree from
+``csrc/`` (see ``include/stellar_sigverify.h``).  This module is a thin ctypes
+binding used by the tests and ``bench.py``; the C++ integration surface that
+mirrors the reference interface (``stellar::PubKeyUtils::verifySig`` /
+``verifySigBatch``, /root/reference/src/crypto/SecretKey.{h,cpp}) lives in
+``csrc/host/``.
+
+There is deliberately no CPU fallback here: if the HIP library is missing or
+no device is present, every entry point raises.
+
+Import it as ``importlib.import_module("stellar-core_amd")`` (the directory
+name follows the repository layout contract; it is not a valid identifier).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libstellar_sigverify.so")
+HOSTLIB_PATH = os.path.join(_HERE, "libstellar_host.so")
+
+SV_OK = 0
+SV_ERRORS = {
+    -1: "SV_ERR_INVALID_ARG",
+    -2: "SV_ERR_NO_DEVICE",
+    -3: "SV_ERR_HIP",
+    -4: "SV_ERR_ALLOC",
+    -5: "SV_ERR_NOT_INIT",
+    -6: "SV_ERR_ALIGN",
+}
+
+EXPORTED_SYMBOLS = (
+    "sv_init", "sv_shutdown", "sv_device_count", "sv_last_error_string", "sv_version",
+    "sv_ed25519_verify_batch", "sv_ed25519_verify_batch_fixed", "sv_ed25519_verify_device",
+    "sv_ed25519_sign_device", "sv_timing_enable", "sv_kernel_time", "sv_kernel_time_reset",
+    "sv_device_synchronize",
+)
+
+
+class SigVerifyError(RuntimeError):
+    """A device/allocation error.  Never a reject: the batch is unverified."""
+
+
+class sv_opts(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32),
+                ("max_devices", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def _share_hip_runtime_with_torch() -> None:
+    # torch ships its own libamdhip64 (soname libamdhip64.so.7).  Importing it
+    # first makes this library bind to that same runtime instead of loading a
+    # second copy from /opt/rocm when torch is (or will be) in the process.
+    if os.environ.get("SV_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SigVerifyError(
+            "libstellar_sigverify.so not built (%s); run __graft_entry__.build() "
+            "or make -C stellar-core_amd" % path)
+    _share_hip_runtime_with_torch()
+    lib = ctypes.CDLL(path)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    lib.sv_init.restype = ctypes.c_int
+    lib.sv_device_count.restype = ctypes.c_int
+    lib.sv_last_error_string.restype = ctypes.c_char_p
+    lib.sv_version.restype = ctypes.c_char_p
+    lib.sv_ed25519_verify_batch.argtypes = [vp, vp, vp, vp, vp, sz, vp, vp]
+    lib.sv_ed25519_verify_batch_fixed.argtypes = [vp, vp, vp, ctypes.c_uint32, sz, vp, vp]
+    lib.sv_ed25519_verify_device.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_uint32, sz, vp, vp, vp]
+    lib.sv_ed25519_sign_device.argtypes = [ctypes.c_int, vp, vp, sz, vp, vp, vp]
+    lib.sv_timing_enable.argtypes = [ctypes.c_int]
+    lib.sv_kernel_time.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    lib.sv_device_synchronize.argtypes = [ctypes.c_int]
+    _lib = lib
+    return lib
+
+
+def _check(rc: int) -> None:
+    if rc != SV_OK:
+        msg = _lib.sv_last_error_string().decode(errors="replace") if _lib else ""
+        raise SigVerifyError("%s: %s" % (SV_ERRORS.get(rc, rc), msg))
+
+
+def _ptr(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _opts(device: int = -1, max_devices: int = 0):
+    o = sv_opts(ctypes.sizeof(sv_opts), device, max_devices, 0)
+    return ctypes.byref(o)
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = lib.sv_device_count()
+    if n < 0:
+        _check(n)
+    return n
+
+
+def version() -> str:
+    return load_library().sv_version().decode()
+
+
+def _u8(a, shape_tail: int) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.uint8))
+    return a.reshape(-1, shape_tail)
+
+
+def verify_batch(pk, sig, msg, msg_off, msg_len, device: int = -1, max_devices: int = 0) -> np.ndarray:
+    """Variable-length batch: message i = msg[msg_off[i]:msg_off[i]+msg_len[i]].
+
+    Returns a uint8 verdict array (1 = valid), bit-identical to libsodium's
+    crypto_sign_verify_detached on every row."""
+    lib = load_library()
+    pk = _u8(pk, 32)
+    sig = _u8(sig, 64)
+    n = pk.shape[0]
+    if sig.shape[0] != n:
+        raise ValueError("pk/sig row mismatch")
+    msg = np.ascontiguousarray(np.asarray(msg, dtype=np.uint8).reshape(-1))
+    if msg.size == 0:
+        msg = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(np.asarray(msg_off, dtype=np.uint64))
+    ln = np.ascontiguousarray(np.asarray(msg_len, dtype=np.uint32))
+    if off.shape[0] != n or ln.shape[0] != n:
+        raise ValueError("msg_off/msg_len length mismatch")
+    if n and int((off + ln).max()) > msg.size:
+        raise ValueError("message range out of bounds")
+    out = np.zeros(n, np.uint8)
+    _check(lib.sv_ed25519_verify_batch(_ptr(pk), _ptr(sig), _ptr(msg), _ptr(off), _ptr(ln), n, _ptr(out),
+                                       _opts(device, max_devices)))
+    return out
+
+
+def verify_messages(pk, sig, messages: Sequence[bytes], **kw) -> np.ndarray:
+    lens = np.array([len(m) for m in messages], np.uint32)
+    off = np.zeros(len(messages), np.uint64)
+    if len(messages) > 1:
+        off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(messages), np.uint8) if messages else np.zeros(0, np.uint8)
+    return verify_batch(pk, sig, buf, off, lens, **kw)
+
+
+def verify_fixed(pk, sig, msg, msg_len: int = 32, device: int = -1, max_devices: int = 0) -> np.ndarray:
+    """Fixed-length batch (msg is n x msg_len bytes); msg_len 32 = tx contents hashes."""
+    lib = load_library()
+    pk = _u8(pk, 32)
+    sig = _u8(sig, 64)
+    n = pk.shape[0]
+    msg = np.ascontiguousarray(np.asarray(msg, dtype=np.uint8).reshape(-1))
+    if msg.size != n * msg_len:
+        raise ValueError("msg must hold n * msg_len bytes")
+    if msg.size == 0:
+        msg = np.zeros(1, np.uint8)
+    out = np.zeros(n, np.uint8)
+    _check(lib.sv_ed25519_verify_batch_fixed(_ptr(pk), _ptr(sig), _ptr(msg), msg_len, n, _ptr(out),
+                                             _opts(device, max_devices)))
+    return out
+
+
+def verify_device(device: int, d_pk: int, d_sig: int, d_msg: int, n: int, d_verdict: int,
+                  d_bitmap: int = 0, stream: int = 0, fixed_msg_len: int = 32,
+                  d_msg_off: int = 0, d_msg_len: int = 0) -> None:
+    """Device-resident batch (raw device pointers, e.g. torch tensor data_ptr())."""
+    lib = load_library()
+    _check(lib.sv_ed25519_verify_device(device, d_pk, d_sig, d_msg, d_msg_off or None, d_msg_len or None,
+                                        fixed_msg_len, n, d_verdict, d_bitmap or None, stream or None))
+
+
+def sign_device(device: int, d_seed: int, d_msg32: int, n: int, d_pk: int, d_sig: int, stream: int = 0) -> None:
+    lib = load_library()
+    _check(lib.sv_ed25519_sign_device(device, d_seed, d_msg32, n, d_pk, d_sig, stream or None))
+
+
+def timing_enable(on: bool = True) -> None:
+    _check(load_library().sv_timing_enable(1 if on else 0))
+
+
+def kernel_time(device: int = 0):
+    lib = load_library()
+    ms, la, sg = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib.sv_kernel_time(device, ctypes.byref(ms), ctypes.byref(la), ctypes.byref(sg)))
+    return ms.value, la.value, sg.value
+
+
+def kernel_time_reset() -> None:
+    _check(load_library().sv_kernel_time_reset())
+
+
+def synchronize(device: int = 0) -> None:
+    _check(load_library().sv_device_synchronize(device))

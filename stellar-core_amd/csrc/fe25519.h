@@ -1,0 +1,291 @@
+// GF(2^255 - 19) arithmetic for one lane, written for gfx950 VALU issue.
+//
+// Representation: 10 unsigned limbs held in 32-bit VGPRs, radix 2^25.5
+// (limb i has weight 2^ceil(25.5 i): offsets 0,26,51,77,102,128,153,179,204,230;
+// even limbs 26 bits, odd limbs 25 bits when carried).
+//
+// Why this and not 8 x 32-bit limbs: the microbenchmark in
+// profiles/r01_ubench_imul.txt shows v_mad_u64_u32 issues at the same rate as
+// v_add_co_u32 on gfx950, so cost = instruction count.  With 25.5-bit limbs
+// every product-accumulate is ONE v_mad_u64_u32 into a carry-free 64-bit column
+// sum (no per-product carry flags, no realignment of 64-bit register pairs),
+// followed by a single carry chain per multiply.
+//
+// Bounds vocabulary ("M" = limb bound in units of 2^26 for even / 2^25 for odd
+// limbs):  R  = output of mul/sq/carry (M ~ 1),  fe_add(R,R) -> M2,
+// fe_sub(R,R) -> M3.  fe_mul/fe_sq accept inputs up to M3 (19 * 3 * 2^26 <
+// 2^32 for the premultiplied operand; column sums < 2^62.8).  Callers that
+// form 3-term expressions re-carry with fe_weak() (see ge25519.h).
+//
+// Reference semantics restated: libsodium 1.0.18 fe25519_* as used by
+// crypto_sign_verify_detached (called from stellar-core
+// src/crypto/SecretKey.cpp:461-463).  Only the mathematical result (values
+// mod p and the canonical encoding) is relied on, never the internal layout.
+#pragma once
+
+#include "sv_common.h"
+
+struct fe {
+  uint32_t v[10];
+};
+
+#define SV_M26 0x3ffffffu
+#define SV_M25 0x1ffffffu
+
+SV_HD uint32_t fe_mask(int i) { return (i & 1) ? SV_M25 : SV_M26; }
+SV_HD int fe_width(int i) { return (i & 1) ? 25 : 26; }
+SV_HD int fe_off(int i) { return 26 * ((i + 1) / 2) + 25 * (i / 2); }
+
+SV_HD void fe_0(fe& h) {
+  SV_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = 0;
+}
+SV_HD void fe_1(fe& h) {
+  fe_0(h);
+  h.v[0] = 1;
+}
+
+// h = f + g
+SV_HD void fe_add(fe& h, const fe& f, const fe& g) {
+  SV_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] + g.v[i];
+}
+
+// h = f - g + 2p; requires g <= R (limbs within 2p's limbs)
+SV_HD void fe_sub(fe& h, const fe& f, const fe& g) {
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    const uint32_t b = (i == 0) ? 0x7ffffdau : ((i & 1) ? 0x3fffffeu : 0x7fffffeu);
+    h.v[i] = f.v[i] + b - g.v[i];
+  }
+}
+
+// h = f - g + 4p; requires g <= M3
+SV_HD void fe_sub4(fe& h, const fe& f, const fe& g) {
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    const uint32_t b = (i == 0) ? 0xfffffb4u : ((i & 1) ? 0x7fffffcu : 0xffffffcu);
+    h.v[i] = f.v[i] + b - g.v[i];
+  }
+}
+
+// h = -f (= 2p - f); requires f <= R
+SV_HD void fe_neg(fe& h, const fe& f) {
+  fe z;
+  fe_0(z);
+  fe_sub(h, z, f);
+}
+
+// Parallel one-round carry: every limb keeps its low width bits and receives
+// the carry of its neighbour (limb 0 receives 19 * carry of limb 9).  For
+// inputs with limbs < 2^31 the output is R+ (limbs <= 2^26 + 2^6 / 2^25 + 2^6,
+// limb 0 <= 2^26 + 19 * 2^6): accepted wherever R is.
+SV_HD void fe_weak(fe& h) {
+  uint32_t c[10];
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    c[i] = h.v[i] >> fe_width(i);
+    h.v[i] &= fe_mask(i);
+  }
+  h.v[0] += 19u * c[9];
+  SV_UNROLL for (int i = 1; i < 10; ++i) h.v[i] += c[i - 1];
+}
+
+// Sequential carry of 64-bit column sums into a carried fe (R).
+// Order interleaves two chains for ILP (0->1->2->3->4 and 4->5->...->9->0).
+SV_HD void fe_carry_wide(fe& out, uint64_t h[10]) {
+  uint64_t c;
+  c = h[0] >> 26; h[1] += c; h[0] &= SV_M26;
+  c = h[4] >> 26; h[5] += c; h[4] &= SV_M26;
+  c = h[1] >> 25; h[2] += c; h[1] &= SV_M25;
+  c = h[5] >> 25; h[6] += c; h[5] &= SV_M25;
+  c = h[2] >> 26; h[3] += c; h[2] &= SV_M26;
+  c = h[6] >> 26; h[7] += c; h[6] &= SV_M26;
+  c = h[3] >> 25; h[4] += c; h[3] &= SV_M25;
+  c = h[7] >> 25; h[8] += c; h[7] &= SV_M25;
+  c = h[4] >> 26; h[5] += c; h[4] &= SV_M26;
+  c = h[8] >> 26; h[9] += c; h[8] &= SV_M26;
+  c = h[9] >> 25; h[0] += c * 19u; h[9] &= SV_M25;
+  c = h[0] >> 26; h[1] += c; h[0] &= SV_M26;
+  SV_UNROLL for (int i = 0; i < 10; ++i) out.v[i] = (uint32_t)h[i];
+}
+
+// Column sums of f*g (DBL: of 2*f*g).  Wrapped columns (i+j >= 10) carry the
+// factor 2^255 = 19 on g; odd*odd products carry an extra 2 (half-bit radix).
+template <bool DBL>
+SV_HD void fe_mul_cols(uint64_t h[10], const fe& f, const fe& g) {
+  uint32_t g19[10], fa[10], fb[10];
+  SV_UNROLL for (int j = 0; j < 10; ++j) g19[j] = 19u * g.v[j];
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    fa[i] = DBL ? (f.v[i] << 1) : f.v[i];       // multiplier when not odd*odd
+    fb[i] = DBL ? (f.v[i] << 2) : (f.v[i] << 1);  // multiplier for odd*odd
+  }
+  SV_UNROLL for (int k = 0; k < 10; ++k) h[k] = 0;
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    SV_UNROLL for (int j = 0; j < 10; ++j) {
+      const int k = i + j;
+      const uint32_t a = ((i & 1) && (j & 1)) ? fb[i] : fa[i];
+      const uint32_t b = (k >= 10) ? g19[j] : g.v[j];
+      h[k >= 10 ? k - 10 : k] += (uint64_t)a * b;
+    }
+  }
+}
+
+// Column sums of f^2 (DBL: 2 f^2), using the symmetry f_i f_j = f_j f_i.
+template <bool DBL>
+SV_HD void fe_sq_cols(uint64_t h[10], const fe& f) {
+  SV_UNROLL for (int k = 0; k < 10; ++k) h[k] = 0;
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    SV_UNROLL for (int j = i; j < 10; ++j) {
+      const int k = i + j;
+      const int sh = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + (DBL ? 1 : 0);
+      const uint32_t a = f.v[i] << sh;
+      const uint32_t b = (k >= 10) ? 19u * f.v[j] : f.v[j];
+      h[k >= 10 ? k - 10 : k] += (uint64_t)a * b;
+    }
+  }
+}
+
+SV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
+  uint64_t c[10];
+  fe_mul_cols<false>(c, f, g);
+  fe_carry_wide(h, c);
+  SV_FENCE();
+}
+// h = 2 f g (doubling folded into the operand; inputs must be <= R)
+SV_HD void fe_mul2(fe& h, const fe& f, const fe& g) {
+  uint64_t c[10];
+  fe_mul_cols<true>(c, f, g);
+  fe_carry_wide(h, c);
+  SV_FENCE();
+}
+SV_HD void fe_sq(fe& h, const fe& f) {
+  uint64_t c[10];
+  fe_sq_cols<false>(c, f);
+  fe_carry_wide(h, c);
+  SV_FENCE();
+}
+// h = 2 f^2 (input must be <= R)
+SV_HD void fe_sq2(fe& h, const fe& f) {
+  uint64_t c[10];
+  fe_sq_cols<true>(c, f);
+  fe_carry_wide(h, c);
+  SV_FENCE();
+}
+// n successive squarings (rolled loop: keeps the code object small)
+SV_HD void fe_sqn(fe& h, const fe& f, int n) {
+  fe_sq(h, f);
+  SV_NOUNROLL for (int i = 1; i < n; ++i) fe_sq(h, h);
+}
+
+// h = cond ? f : h  (per lane, branch-free)
+SV_HD void fe_cmov(fe& h, const fe& f, bool cond) {
+  SV_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = cond ? f.v[i] : h.v[i];
+}
+
+// 255-bit little-endian value (bit 255 ignored, value may be >= p) -> fe
+SV_HD void fe_frombytes(fe& h, const uint32_t w[8]) {
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    const int o = fe_off(i), q = o >> 5, r = o & 31;
+    uint32_t x = w[q] >> r;
+    if (r + fe_width(i) > 32) x |= w[q + 1] << (32 - r);
+    h.v[i] = x & fe_mask(i);
+  }
+}
+
+// canonical little-endian encoding (value mod p, < p) as 8 words
+SV_COLD void fe_tobytes(uint32_t out[8], const fe& f) {
+  uint32_t h[10];
+  SV_UNROLL for (int i = 0; i < 10; ++i) h[i] = f.v[i];
+  // three sequential carry passes: limbs within width, value < 2^255
+  SV_UNROLL for (int pass = 0; pass < 3; ++pass) {
+    SV_UNROLL for (int i = 0; i < 9; ++i) {
+      h[i + 1] += h[i] >> fe_width(i);
+      h[i] &= fe_mask(i);
+    }
+    const uint32_t c = h[9] >> 25;
+    h[9] &= SV_M25;
+    h[0] += 19u * c;
+  }
+  // q = [value >= p] = [value + 19 >= 2^255]
+  uint32_t q = (h[0] + 19u) >> 26;
+  SV_UNROLL for (int i = 1; i < 10; ++i) q = (h[i] + q) >> fe_width(i);
+  h[0] += 19u * q;
+  SV_UNROLL for (int i = 0; i < 9; ++i) {
+    h[i + 1] += h[i] >> fe_width(i);
+    h[i] &= fe_mask(i);
+  }
+  h[9] &= SV_M25;  // drops 2^255 (i.e. subtracts p together with the +19)
+  SV_UNROLL for (int w = 0; w < 8; ++w) out[w] = 0;
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    const int o = fe_off(i), q2 = o >> 5, r = o & 31;
+    out[q2] |= h[i] << r;
+    if (r + fe_width(i) > 32) out[q2 + 1] |= h[i] >> (32 - r);
+  }
+}
+
+SV_HD bool fe_iszero(const fe& f) {
+  uint32_t s[8];
+  fe_tobytes(s, f);
+  uint32_t acc = 0;
+  SV_UNROLL for (int i = 0; i < 8; ++i) acc |= s[i];
+  return acc == 0;
+}
+SV_HD uint32_t fe_isnegative(const fe& f) {
+  uint32_t s[8];
+  fe_tobytes(s, f);
+  return s[0] & 1u;
+}
+
+// z^(2^250 - 1) and the two small powers the chains below need.
+SV_COLD void fe_pow_2_250_1(fe& z250, fe& z11, const fe& z) {
+  fe t0, t1, t2, z9, z_5_0, z_10_0, z_20_0, z_50_0, z_100_0;
+  fe_sq(t0, z);              // z^2
+  fe_sqn(t1, t0, 2);         // z^8
+  fe_mul(z9, t1, z);         // z^9
+  fe_mul(z11, z9, t0);       // z^11
+  fe_sq(t2, z11);            // z^22
+  fe_mul(z_5_0, t2, z9);     // z^31 = z^(2^5-1)
+  fe_sqn(t0, z_5_0, 5);
+  fe_mul(z_10_0, t0, z_5_0);   // 2^10-1
+  fe_sqn(t0, z_10_0, 10);
+  fe_mul(z_20_0, t0, z_10_0);  // 2^20-1
+  fe_sqn(t0, z_20_0, 20);
+  fe_mul(t0, t0, z_20_0);      // 2^40-1
+  fe_sqn(t0, t0, 10);
+  fe_mul(z_50_0, t0, z_10_0);  // 2^50-1
+  fe_sqn(t0, z_50_0, 50);
+  fe_mul(z_100_0, t0, z_50_0); // 2^100-1
+  fe_sqn(t0, z_100_0, 100);
+  fe_mul(t0, t0, z_100_0);     // 2^200-1
+  fe_sqn(t0, t0, 50);
+  fe_mul(z250, t0, z_50_0);    // 2^250-1
+}
+
+// z^((p-5)/8) = z^(2^252 - 3)
+SV_COLD void fe_pow22523(fe& h, const fe& z) {
+  fe z250, z11;
+  fe_pow_2_250_1(z250, z11, z);
+  fe_sqn(z250, z250, 2);
+  fe_mul(h, z250, z);
+}
+
+// z^(p-2) = z^(2^255 - 21)
+SV_COLD void fe_invert(fe& h, const fe& z) {
+  fe z250, z11;
+  fe_pow_2_250_1(z250, z11, z);
+  fe_sqn(z250, z250, 5);
+  fe_mul(h, z250, z11);
+}
+
+// curve constants (tools/gen_constants.py, radix 2^25.5)
+SV_HD void fe_const_d(fe& h) {
+  const uint32_t c[10] = {0x35978a3, 0x0d37284, 0x3156ebd, 0x06a0a0e, 0x001c029,
+                          0x179e898, 0x3a03cbb, 0x1ce7198, 0x2e2b6ff, 0x1480db3};
+  SV_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = c[i];
+}
+SV_HD void fe_const_2d(fe& h) {
+  const uint32_t c[10] = {0x2b2f159, 0x1a6e509, 0x22add7a, 0x0d4141d, 0x0038052,
+                          0x0f3d130, 0x3407977, 0x19ce331, 0x1c56dff, 0x0901b67};
+  SV_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = c[i];
+}
+SV_HD void fe_const_sqrtm1(fe& h) {
+  const uint32_t c[10] = {0x20ea0b0, 0x186c9d2, 0x08f189d, 0x035697f, 0x0bd0c60,
+                          0x1fbd7a7, 0x2804c9e, 0x1e16569, 0x004fc1d, 0x0ae0c92};
+  SV_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = c[i];
+}

@@ -1,0 +1,34 @@
+// Shared qualifiers for the device arithmetic headers.
+//
+// The arithmetic headers are written once and compiled for gfx950 by hipcc.
+// tests/native/ also compiles them for the host with g++ (SV_HOST_TEST) so the
+// limb-bound reasoning can be fuzzed on CPU against Python big integers; that
+// host build is test infrastructure only and is never linked into the product.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define SV_HD __host__ __device__ __forceinline__
+// Once-per-signature phases (exponentiation chains, decompression, SHA-512,
+// mod-L reduction): instantiated once as device functions instead of being
+// inlined at every call site, to keep the code object within the I-cache.
+#define SV_COLD __host__ __device__ __noinline__
+#define SV_CONST __constant__
+#else
+#define SV_HD static inline
+#define SV_COLD static
+#define SV_CONST static const
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// Keeps the scheduler from interleaving independent field operations, which
+// otherwise multiplies their live ranges and spills VGPRs.
+#define SV_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SV_FENCE() ((void)0)
+#endif
+
+#define SV_UNROLL _Pragma("unroll")
+#define SV_NOUNROLL _Pragma("unroll 1")

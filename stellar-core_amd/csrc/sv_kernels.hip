@@ -1,0 +1,184 @@
+// gfx950 kernels of the batched ed25519 verification engine.
+//
+// One lane verifies one signature (the per-lane algorithm is verify_core.h).
+// Grid: persistent, gridDim = CUs x resident workgroups per CU; each wave
+// walks the batch in wave-uniform strides of (grid threads), so lanes of a
+// wave always hold 64 consecutive signatures (coalesced SoA loads, one
+// ballot word of the verdict bitmap per wave iteration).
+//
+// Memory per workgroup: the 129-entry base-point table (18.6 KiB) in LDS.
+// Memory per lane: a 1440 B slot of the HBM workspace for the signature's
+// 9-entry table of multiples of -A, interleaved so that quad q of entry e of
+// the 64 lanes of a wave is one contiguous 1 KiB line.
+#include <hip/hip_runtime.h>
+
+#include "verify_core.h"
+
+#define SV_BLOCK 256
+#define SV_WAVES_PER_SIMD 2
+
+struct sv_kparams {
+  const sv_u4* pk;        // n x 32 B (2 quads)
+  const sv_u4* sig;       // n x 64 B (4 quads)
+  const uint8_t* msg;     // fixed: n x fixed_len ; var: msg bytes
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  uint64_t n;
+  uint32_t fixed_len;     // 0 = variable-length
+  uint8_t* verdict;       // n bytes
+  uint64_t* bitmap;       // optional, ceil(n/64) words
+  sv_u4* ws;              // workspace: (grid threads / 64) x 9 x 10 x 64 quads
+  const sv_u4* btab;      // SV_BTAB_ENTRIES x 9 quads (global copy)
+};
+
+__device__ __forceinline__ void sv_load_btab_lds(sv_u4* s_btab, const sv_u4* g_btab) {
+  for (int i = threadIdx.x; i < SV_BTAB_ENTRIES * (SV_BTAB_STRIDE / 4); i += blockDim.x) s_btab[i] = g_btab[i];
+  __syncthreads();
+}
+
+__device__ __forceinline__ void sv_unpack2(uint32_t w[8], const sv_u4* p) {
+  const sv_u4 a = p[0], b = p[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+template <int MODE>  // 0: fixed 32-byte messages, 1: variable length, 2: fixed other length
+__global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_kernel(sv_kparams p) {
+  __shared__ sv_u4 s_btab[SV_BTAB_ENTRIES * (SV_BTAB_STRIDE / 4)];
+  sv_load_btab_lds(s_btab, p.btab);
+
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t wave = gtid >> 6;
+  sv_u4* slot = p.ws + wave * (SV_ATAB_ENTRIES * SV_ATAB_QUADS * 64) + lane;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+
+  for (uint64_t base = gtid - lane; base < p.n; base += stride) {
+    const uint64_t i = base + lane;
+    const bool active = i < p.n;
+    const uint64_t ii = active ? i : p.n - 1;  // idle tail lanes redo the last item
+    uint32_t A[8], R[8], S[8], hram[16];
+    sv_unpack2(A, p.pk + 2 * ii);
+    sv_unpack2(R, p.sig + 4 * ii);
+    sv_unpack2(S, p.sig + 4 * ii + 2);
+    if (MODE == 0) {
+      uint32_t M[8];
+      sv_unpack2(M, (const sv_u4*)(p.msg) + 2 * ii);
+      sha512_ram32(hram, R, A, M);
+    } else if (MODE == 1) {
+      sha512_ram_var(hram, R, A, p.msg + p.msg_off[ii], p.msg_len[ii]);
+    } else {
+      sha512_ram_var(hram, R, A, p.msg + ii * (uint64_t)p.fixed_len, p.fixed_len);
+    }
+    const bool ok = sv_verify_core(A, p.sig + 4 * ii, S, hram, slot, 64, s_btab) && active;
+    if (active) p.verdict[i] = ok ? 1 : 0;
+    const uint64_t mask = __ballot(ok);
+    if (p.bitmap != nullptr && lane == 0) p.bitmap[base >> 6] = mask;
+  }
+}
+
+__global__ void sv_btab_init_kernel(uint32_t* btab) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < SV_BTAB_ENTRIES) sv_btab_entry(btab + e * SV_BTAB_STRIDE, e);
+}
+
+struct sv_sparams {
+  const sv_u4* seed;  // n x 32 B
+  const sv_u4* msg;   // n x 32 B
+  uint64_t n;
+  sv_u4* pk;          // n x 32 B out
+  sv_u4* sig;         // n x 64 B out
+  sv_u4* ws;
+  const sv_u4* btab;
+};
+
+__global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_sign_kernel(sv_sparams p) {
+  __shared__ sv_u4 s_btab[SV_BTAB_ENTRIES * (SV_BTAB_STRIDE / 4)];
+  sv_load_btab_lds(s_btab, p.btab);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  sv_u4* slot = p.ws + (gtid >> 6) * (SV_ATAB_ENTRIES * SV_ATAB_QUADS * 64) + lane;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = gtid - lane; base < p.n; base += stride) {
+    const uint64_t i = base + lane;
+    const bool active = i < p.n;
+    const uint64_t ii = active ? i : p.n - 1;
+    uint32_t seed[8], M[8], pk[8], sig[16];
+    sv_unpack2(seed, p.seed + 2 * ii);
+    sv_unpack2(M, p.msg + 2 * ii);
+    sv_sign_lane(pk, sig, seed, M, slot, 64, s_btab);
+    if (active) {
+      p.pk[2 * i] = sv_u4{pk[0], pk[1], pk[2], pk[3]};
+      p.pk[2 * i + 1] = sv_u4{pk[4], pk[5], pk[6], pk[7]};
+      SV_UNROLL for (int q = 0; q < 4; ++q)
+        p.sig[4 * i + q] = sv_u4{sig[4 * q], sig[4 * q + 1], sig[4 * q + 2], sig[4 * q + 3]};
+    }
+  }
+}
+
+// ------------------------------------------------------------ launchers
+extern "C" {
+
+size_t sv_ws_bytes_per_block(void) {
+  return (size_t)(SV_BLOCK / 64) * SV_ATAB_ENTRIES * SV_ATAB_QUADS * 64 * sizeof(sv_u4);
+}
+size_t sv_btab_bytes(void) { return (size_t)SV_BTAB_DWORDS * 4; }
+int sv_block_threads(void) { return SV_BLOCK; }
+
+hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s) {
+  hipLaunchKernelGGL(sv_btab_init_kernel, dim3(1), dim3(192), 0, s, d_btab);
+  return hipGetLastError();
+}
+
+int sv_occupancy_blocks_per_cu(void) {
+  int b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, sv_verify_kernel<0>, SV_BLOCK, 0) != hipSuccess) b0 = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, sv_verify_kernel<1>, SV_BLOCK, 0) != hipSuccess) b1 = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, sv_verify_kernel<2>, SV_BLOCK, 0) != hipSuccess) b2 = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b3, sv_sign_kernel, SV_BLOCK, 0) != hipSuccess) b3 = 1;
+  int m = b0;
+  if (b1 > m) m = b1;
+  if (b2 > m) m = b2;
+  if (b3 > m) m = b3;
+  return m < 1 ? 1 : m;
+}
+
+hipError_t sv_launch_verify(int mode, unsigned grid, const void* pk, const void* sig, const void* msg,
+                            const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n,
+                            void* verdict, void* bitmap, void* ws, const void* btab, hipStream_t s) {
+  sv_kparams p;
+  p.pk = (const sv_u4*)pk;
+  p.sig = (const sv_u4*)sig;
+  p.msg = (const uint8_t*)msg;
+  p.msg_off = off;
+  p.msg_len = len;
+  p.n = n;
+  p.fixed_len = fixed_len;
+  p.verdict = (uint8_t*)verdict;
+  p.bitmap = (uint64_t*)bitmap;
+  p.ws = (sv_u4*)ws;
+  p.btab = (const sv_u4*)btab;
+  if (mode == 0)
+    hipLaunchKernelGGL(sv_verify_kernel<0>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
+  else if (mode == 1)
+    hipLaunchKernelGGL(sv_verify_kernel<1>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
+  else
+    hipLaunchKernelGGL(sv_verify_kernel<2>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t sv_launch_sign(unsigned grid, const void* seed, const void* msg, uint64_t n, void* pk, void* sig,
+                          void* ws, const void* btab, hipStream_t s) {
+  sv_sparams p;
+  p.seed = (const sv_u4*)seed;
+  p.msg = (const sv_u4*)msg;
+  p.n = n;
+  p.pk = (sv_u4*)pk;
+  p.sig = (sv_u4*)sig;
+  p.ws = (sv_u4*)ws;
+  p.btab = (const sv_u4*)btab;
+  hipLaunchKernelGGL(sv_sign_kernel, dim3(grid), dim3(SV_BLOCK), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // extern "C"

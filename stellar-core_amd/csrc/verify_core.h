@@ -1,0 +1,287 @@
+// Per-lane ed25519 verification core (one lane = one signature).
+//
+// Accept/reject is bit-exact with libsodium 1.0.18 crypto_sign_verify_detached,
+// the function stellar-core's PubKeyUtils::verifySig calls on a cache miss
+// (/root/reference/src/crypto/SecretKey.cpp:461-463).  Steps, in libsodium's
+// order (all evaluated branch-free per lane; the verdict is their AND):
+//   (1) S < L                              sc_is_canonical
+//   (2) R not one of 7 small-order encodings (bit 255 masked)
+//   (3) A canonical (y < p, sign ignored)   (4) A not small-order
+//   (5) -A = decompress(A) succeeds
+//   (6) h = SHA-512(R || A || M) mod L      (computed by the caller)
+//   (7) R' = [h](-A) + [S]B, cofactorless
+//   (8) encode(R') == R byte-for-byte
+//
+// Step (7) schedule (wave-uniform, no per-lane branches):
+//   64 windows of 4 bits.  Per window: 4 doublings; add table_A[d_A] with
+//   d_A in [-8, 7] (signed radix 16 of h); on even windows also add
+//   table_B[d_B], d_B in [-128, 127] (signed radix 256 of S).
+//   table_A = {0..8}·(-A) in cached form, built per lane into an HBM workspace
+//   slot (1440 B/lane, too big for LDS at >=2 waves/SIMD);
+//   table_B = {0..128}·B in affine precomp form, shared by the workgroup in LDS.
+//   Zero digits add the identity entry, so every lane does identical work.
+#pragma once
+
+#include "ge25519.h"
+#include "sc25519.h"
+#include "sha512_dev.h"
+
+struct __attribute__((aligned(16))) sv_u4 {
+  uint32_t x, y, z, w;
+};
+
+// Every table field element is padded to 12 dwords (3 quads) so a negative
+// digit's (Y+X) <-> (Y-X) swap is an address choice at load time.
+// B-table (LDS / global): entry e = 36 dwords: ypx[12] ymx[12] xy2d[12]
+#define SV_BTAB_ENTRIES 129
+#define SV_BTAB_STRIDE 36
+#define SV_BTAB_DWORDS (SV_BTAB_ENTRIES * SV_BTAB_STRIDE)
+// A-table (HBM workspace): 9 entries x 12 quads: YpX YmX Z T2d (3 quads each)
+#define SV_ATAB_ENTRIES 9
+#define SV_ATAB_QUADS 12
+
+SV_HD bool sv_small_order(const uint32_t s[8]) {
+  const uint32_t bl[7][8] = {
+      {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+      {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+      {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du},
+      {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u},
+      {0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+      {0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+      {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu}};
+  bool hit = false;
+  SV_UNROLL for (int k = 0; k < 7; ++k) {
+    uint32_t diff = (s[7] & 0x7fffffffu) ^ bl[k][7];
+    SV_UNROLL for (int i = 0; i < 7; ++i) diff |= s[i] ^ bl[k][i];
+    hit |= (diff == 0);
+  }
+  return hit;
+}
+
+// y < p with the sign bit ignored (libsodium ge25519_is_canonical)
+SV_HD bool sv_point_canonical(const uint32_t s[8]) {
+  uint32_t ones = (s[7] & 0x7fffffffu) ^ 0x7fffffffu;
+  SV_UNROLL for (int i = 1; i < 7; ++i) ones |= s[i] ^ 0xffffffffu;
+  return !(ones == 0 && s[0] >= 0xffffffedu);
+}
+
+SV_HD void sv_store_fe3(sv_u4* p, int qstride, const fe& f) {
+  p[0] = sv_u4{f.v[0], f.v[1], f.v[2], f.v[3]};
+  p[qstride] = sv_u4{f.v[4], f.v[5], f.v[6], f.v[7]};
+  p[2 * qstride] = sv_u4{f.v[8], f.v[9], 0u, 0u};
+}
+SV_HD void sv_load_fe3(fe& f, const sv_u4* p, int qstride) {
+  const sv_u4 a = p[0], b = p[qstride], c = p[2 * qstride];
+  f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+  f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+  f.v[8] = c.x; f.v[9] = c.y;
+}
+
+SV_HD void sv_store_cached(sv_u4* slot, int qstride, int e, const ge_cached& c) {
+  sv_u4* base = slot + e * SV_ATAB_QUADS * qstride;
+  sv_store_fe3(base, qstride, c.YpX);
+  sv_store_fe3(base + 3 * qstride, qstride, c.YmX);
+  sv_store_fe3(base + 6 * qstride, qstride, c.Z);
+  sv_store_fe3(base + 9 * qstride, qstride, c.T2d);
+}
+
+// table_A = {0..8}·(-A) in cached form, written to the lane's workspace slot.
+SV_COLD void sv_build_atab(sv_u4* slot, int qstride, const ge_p3& negA) {
+  ge_cached c1, ce;
+  ge_p3_to_cached(c1, negA);
+  ge_cached_identity(ce);
+  sv_store_cached(slot, qstride, 0, ce);
+  sv_store_cached(slot, qstride, 1, c1);
+  ge_p3 P3 = negA;
+  ge_p1p1 Q;
+  SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
+    ge_add_any<false>(Q, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false);
+    ge_p1p1_to_p3(P3, Q);
+    ge_p3_to_cached(ce, P3);
+    sv_store_cached(slot, qstride, e, ce);
+  }
+}
+
+// Builds table_A for -A in the lane's workspace slot and computes
+// enc = encode([h](-A) + [S]B)  (step (7) and the encoding half of (8)).
+//
+// Step machine: per window w (64 of them, MSB first) run steps
+//   s = 0..3  doubling, s = 4  add table_A[d_A], s = 5 (even w) add table_B[d_B]
+// with one code instance of each step kind; every branch is wave-uniform.
+SV_HD void sv_double_scalarmult_encode(uint32_t enc[8], const ge_p3& negA, const uint32_t h[8],
+                                       const uint32_t S[8], sv_u4* slot, int qstride,
+                                       const sv_u4* btab) {
+  sv_build_atab(slot, qstride, negA);
+
+  uint32_t da[8], db[8];
+  sc_digits_r16(da, h);
+  sc_digits_r256(db, S);
+
+  ge_p3 P;
+  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
+  ge_p1p1 Q;
+  SV_NOUNROLL for (int w = 63; w >= 0; --w) {
+    const int nsteps = (w & 1) ? 5 : 6;
+    SV_NOUNROLL for (int s = 0; s < nsteps; ++s) {
+      if (s < 4) {
+        ge_dbl(Q, P.X, P.Y, P.Z);
+      } else {
+        fe qa, qb, qz, qt;
+        bool neg;
+        if (s == 4) {
+          const int32_t d = sc_pop_top(da, 4);
+          neg = d < 0;
+          const sv_u4* e = slot + (neg ? -d : d) * SV_ATAB_QUADS * qstride;
+          sv_load_fe3(qa, e + (neg ? 3 : 0) * qstride, qstride);
+          sv_load_fe3(qb, e + (neg ? 0 : 3) * qstride, qstride);
+          sv_load_fe3(qz, e + 6 * qstride, qstride);
+          sv_load_fe3(qt, e + 9 * qstride, qstride);
+        } else {
+          const int32_t d = sc_pop_top(db, 8);
+          neg = d < 0;
+          const sv_u4* e = btab + (neg ? -d : d) * (SV_BTAB_STRIDE / 4);
+          sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
+          sv_load_fe3(qb, e + (neg ? 0 : 3), 1);
+          fe_1(qz);
+          sv_load_fe3(qt, e + 6, 1);
+        }
+        ge_add_preswapped(Q, P, qa, qb, qz, qt, neg);
+      }
+      ge_p1p1_to_p3_opt(P, Q, s + 1 >= 4 && s + 1 < nsteps);
+    }
+  }
+  ge_p2_tobytes(enc, P.X, P.Y, P.Z);
+}
+
+// Steps (1)-(8) given the SHA-512(R||A||M) digest as a 512-bit LE integer.
+// R is read twice from memory (Rp: its 2 quads) rather than kept live in
+// VGPRs across the scalar multiplication.
+SV_HD bool sv_verify_core(const uint32_t A[8], const sv_u4* Rp, const uint32_t S[8],
+                          const uint32_t hram[16], sv_u4* slot, int qstride, const sv_u4* btab) {
+  bool ok;
+  {
+    uint32_t R[8];
+    const sv_u4 r0 = Rp[0], r1 = Rp[1];
+    R[0] = r0.x; R[1] = r0.y; R[2] = r0.z; R[3] = r0.w;
+    R[4] = r1.x; R[5] = r1.y; R[6] = r1.z; R[7] = r1.w;
+    ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A);
+  }
+  ge_p3 negA;
+  ok = ge_frombytes(negA, A, true) && ok;
+  uint32_t h[8];
+  sc_reduce512(h, hram);
+  // Lanes with S >= L are already rejected by (1); masking S's top nibble keeps
+  // their radix-256 recoding inside [-128, 127] (table bounds).  For every
+  // lane that can be accepted (S < L < 2^253) the mask is a no-op.
+  uint32_t Sc[8];
+  SV_UNROLL for (int i = 0; i < 8; ++i) Sc[i] = S[i];
+  Sc[7] &= 0x0fffffffu;
+  uint32_t enc[8];
+  sv_double_scalarmult_encode(enc, negA, h, Sc, slot, qstride, btab);
+  const sv_u4 r0 = Rp[0], r1 = Rp[1];
+  const uint32_t diff = (enc[0] ^ r0.x) | (enc[1] ^ r0.y) | (enc[2] ^ r0.z) | (enc[3] ^ r0.w) |
+                        (enc[4] ^ r1.x) | (enc[5] ^ r1.y) | (enc[6] ^ r1.z) | (enc[7] ^ r1.w);
+  return ok && diff == 0;
+}
+
+// Base-point table entry e = e·B in affine precomp form (used at init).
+// Computes e·B by double-and-add from B (e <= 128) and normalises.
+SV_HD void sv_btab_entry(uint32_t out[SV_BTAB_STRIDE], int e) {
+  const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                            0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+  ge_p3 B, acc;
+  ge_frombytes(B, benc, false);
+  ge_cached bc;
+  ge_p3_to_cached(bc, B);
+  // acc = identity
+  fe_0(acc.X); fe_1(acc.Y); fe_1(acc.Z); fe_0(acc.T);
+  ge_p1p1 Q;
+  for (int i = 0; i < e; ++i) {
+    ge_add_any<false>(Q, acc, bc.YpX, bc.YmX, bc.Z, bc.T2d, false);
+    ge_p1p1_to_p3(acc, Q);
+  }
+  fe zi, x, y, xy, d2, ypx, ymx, xy2d;
+  fe_invert(zi, acc.Z);
+  fe_mul(x, acc.X, zi);
+  fe_mul(y, acc.Y, zi);
+  fe_mul(xy, x, y);
+  fe_const_2d(d2);
+  fe_mul(xy2d, xy, d2);
+  fe_add(ypx, y, x);
+  fe_weak(ypx);
+  fe_sub(ymx, y, x);
+  fe_weak(ymx);
+  for (int i = 0; i < SV_BTAB_STRIDE; ++i) out[i] = 0;
+  for (int i = 0; i < 10; ++i) {
+    out[i] = ypx.v[i];
+    out[12 + i] = ymx.v[i];
+    out[24 + i] = xy2d.v[i];
+  }
+}
+
+// ---------------------------------------------------------------- signing
+// RFC 8032 deterministic signing (== libsodium crypto_sign_seed_keypair +
+// crypto_sign_detached), used only to synthesise benchmark datasets on the
+// device.  [k]B runs through the same double-scalar routine with h = 0 (every
+// table_A digit is 0, so only the identity entry is read).
+
+// one-block SHA-512 of NW little-endian-packed words (NW*4 <= 111 bytes)
+template <int NW>
+SV_HD void sha512_words(uint32_t out[16], const uint32_t* in) {
+  uint64_t st[8], w[16];
+  sha512_init(st);
+  SV_UNROLL for (int t = 0; t < 16; ++t) w[t] = 0;
+  SV_UNROLL for (int t = 0; t < NW / 2; ++t) w[t] = sv_be64(in[2 * t], in[2 * t + 1]);
+  w[NW / 2] = 0x8000000000000000ULL;
+  w[15] = (uint64_t)NW * 32;
+  sha512_compress(st, w);
+  sha512_digest_le(out, st);
+}
+
+SV_HD void sc_muladd(uint32_t s[8], const uint32_t a[8], const uint32_t b[8], const uint32_t c[8]) {
+  uint32_t x[16];
+  SV_UNROLL for (int i = 0; i < 16; ++i) x[i] = 0;
+  SV_UNROLL for (int i = 0; i < 8; ++i) {
+    uint64_t carry = 0;
+    SV_UNROLL for (int j = 0; j < 8; ++j) {
+      const uint64_t t = (uint64_t)a[i] * b[j] + x[i + j] + carry;
+      x[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    x[i + 8] = (uint32_t)carry;
+  }
+  uint64_t carry = 0;
+  SV_UNROLL for (int i = 0; i < 16; ++i) {
+    const uint64_t t = (uint64_t)x[i] + (i < 8 ? c[i] : 0u) + carry;
+    x[i] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  sc_reduce512(s, x);
+}
+
+SV_HD void sv_sign_lane(uint32_t pk[8], uint32_t sig[16], const uint32_t seed[8], const uint32_t M[8],
+                        sv_u4* slot, int qstride, const sv_u4* btab) {
+  uint32_t az[16], wide[16], a[8], zero[8], enc[8];
+  sha512_words<8>(az, seed);
+  az[0] &= ~7u;
+  az[7] &= 0x7fffffffu;
+  az[7] |= 0x40000000u;
+  SV_UNROLL for (int i = 0; i < 16; ++i) wide[i] = i < 8 ? az[i] : 0u;
+  sc_reduce512(a, wide);
+  SV_UNROLL for (int i = 0; i < 8; ++i) zero[i] = 0;
+  ge_p3 ident;
+  fe_0(ident.X); fe_1(ident.Y); fe_1(ident.Z); fe_0(ident.T);
+  sv_double_scalarmult_encode(enc, ident, zero, a, slot, qstride, btab);  // A = aB
+  SV_UNROLL for (int i = 0; i < 8; ++i) pk[i] = enc[i];
+  uint32_t pm[16], nonce[16], r[8];
+  SV_UNROLL for (int i = 0; i < 8; ++i) { pm[i] = az[8 + i]; pm[8 + i] = M[i]; }
+  sha512_words<16>(nonce, pm);
+  sc_reduce512(r, nonce);
+  sv_double_scalarmult_encode(enc, ident, zero, r, slot, qstride, btab);  // R = rB
+  uint32_t hram[16], h[8];
+  sha512_ram32(hram, enc, pk, M);
+  sc_reduce512(h, hram);
+  uint32_t S[8];
+  sc_muladd(S, h, a, r);
+  SV_UNROLL for (int i = 0; i < 8; ++i) { sig[i] = enc[i]; sig[8 + i] = S[i]; }
+}

@@ -1,0 +1,116 @@
+// TEST INFRASTRUCTURE ONLY: compiles the device arithmetic headers of
+// stellar-core_amd/csrc for the host (g++) so tests can fuzz the field /
+// scalar / point layers and run the per-lane verifier on CPU against the
+// golden fixtures before the GPU run.  Never linked into the product library.
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../stellar-core_amd/csrc/verify_core.h"
+
+static std::vector<uint32_t> g_btab;
+static std::once_flag g_once;
+
+static void init_btab() {
+  g_btab.assign(SV_BTAB_DWORDS + 8, 0);
+  for (int e = 0; e < SV_BTAB_ENTRIES; ++e) sv_btab_entry(&g_btab[e * SV_BTAB_STRIDE], e);
+}
+
+static void load_words(uint32_t w[8], const uint8_t* b) { memcpy(w, b, 32); }
+
+extern "C" {
+
+// field ops on 32-byte little-endian values (value < 2^255 as input)
+void hc_fe_mul(uint8_t out[32], const uint8_t a[32], const uint8_t b[32]) {
+  uint32_t wa[8], wb[8], wo[8];
+  load_words(wa, a); load_words(wb, b);
+  fe fa, fb, fo;
+  fe_frombytes(fa, wa); fe_frombytes(fb, wb);
+  fe_mul(fo, fa, fb);
+  fe_tobytes(wo, fo);
+  memcpy(out, wo, 32);
+}
+
+// raw-limb entry points: limbs given directly (bounds fuzzing)
+void hc_fe_mul_limbs(uint32_t out_bytes[8], const uint32_t a[10], const uint32_t b[10], int dbl) {
+  fe fa, fb, fo;
+  memcpy(fa.v, a, 40); memcpy(fb.v, b, 40);
+  if (dbl) fe_mul2(fo, fa, fb); else fe_mul(fo, fa, fb);
+  fe_tobytes(out_bytes, fo);
+}
+void hc_fe_sq_limbs(uint32_t out_bytes[8], const uint32_t a[10], int dbl) {
+  fe fa, fo;
+  memcpy(fa.v, a, 40);
+  if (dbl) fe_sq2(fo, fa); else fe_sq(fo, fa);
+  fe_tobytes(out_bytes, fo);
+}
+void hc_fe_tobytes_limbs(uint32_t out_bytes[8], const uint32_t a[10]) {
+  fe fa;
+  memcpy(fa.v, a, 40);
+  fe_tobytes(out_bytes, fa);
+}
+void hc_fe_invert(uint8_t out[32], const uint8_t a[32]) {
+  uint32_t wa[8], wo[8];
+  load_words(wa, a);
+  fe fa, fo;
+  fe_frombytes(fa, wa);
+  fe_invert(fo, fa);
+  fe_tobytes(wo, fo);
+  memcpy(out, wo, 32);
+}
+void hc_sc_reduce512(uint8_t out[32], const uint8_t in[64]) {
+  uint32_t x[16], r[8];
+  memcpy(x, in, 64);
+  sc_reduce512(r, x);
+  memcpy(out, r, 32);
+}
+void hc_sha512_ram(uint8_t out[64], const uint8_t R[32], const uint8_t A[32], const uint8_t* m, uint32_t mlen,
+                   int fixed) {
+  uint32_t wr[8], wa[8], h[16];
+  load_words(wr, R); load_words(wa, A);
+  if (fixed) {
+    uint32_t wm[8];
+    memcpy(wm, m, 32);
+    sha512_ram32(h, wr, wa, wm);
+  } else {
+    sha512_ram_var(h, wr, wa, m, mlen);
+  }
+  memcpy(out, h, 64);
+}
+// decompress (negate=0/1): returns ok, writes canonical encoding of the point
+int hc_decompress(uint8_t out[32], const uint8_t s[32], int negate) {
+  uint32_t w[8], e[8];
+  load_words(w, s);
+  ge_p3 p;
+  bool ok = ge_frombytes(p, w, negate != 0);
+  ge_p2_tobytes(e, p.X, p.Y, p.Z);
+  memcpy(out, e, 32);
+  return ok ? 1 : 0;
+}
+void hc_btab(uint32_t* out) {
+  std::call_once(g_once, init_btab);
+  memcpy(out, g_btab.data(), SV_BTAB_DWORDS * 4);
+}
+
+void hc_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                     const uint32_t* len, size_t n, uint8_t* verdict) {
+  std::call_once(g_once, init_btab);
+  std::vector<sv_u4> slot(SV_ATAB_ENTRIES * SV_ATAB_QUADS);
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t A[8], S[8], hram[16];
+    alignas(16) uint32_t R[8];
+    load_words(A, pk + 32 * i);
+    load_words(R, sig + 64 * i);
+    load_words(S, sig + 64 * i + 32);
+    if (len[i] == 32) {
+      uint32_t M[8];
+      memcpy(M, msg + off[i], 32);
+      sha512_ram32(hram, R, A, M);
+    } else {
+      sha512_ram_var(hram, R, A, msg + off[i], len[i]);
+    }
+    verdict[i] = sv_verify_core(A, (const sv_u4*)R, S, hram, slot.data(), 1, (const sv_u4*)g_btab.data()) ? 1 : 0;
+  }
+}
+}
