@@ -1,0 +1,370 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ed25519 verifies/sec @1M batch per GPU + p50 latency @1k batch.
+
+Metric and configs: BASELINE.json.  One "step" = one pass of the hot path
+(sv_ed25519_verify_device) over one batch of 2^20 signatures per GPU, inputs
+already resident in HBM.  N GPUs run as N processes (torchrun), each verifying
+its own contiguous slice of the global index space (weak scaling, no data-path
+collective; the only collectives are the barrier and the max-over-ranks of the
+timed region, over gloo).
+
+Dataset: seed_i = SHA-256("SVSEED"||u64le i), msg_i =
+SHA-256("SVMSG"||u64le i); keypairs and signatures are generated ON THE GPU
+by the engine's RFC 8032 signer, and on rank 0 the SHA-256 of the
+pk||sig||msg stream is compared with the libsodium-generated digest in
+tests/golden/digests.json, so the bench verifies the exact dataset libsodium
+would produce.
+
+Printed by rank 0: one JSON line (contract in the task statement) with
+  roofline      VALU-integer roofline of the verify kernel (kernel time from
+                HIP events on the engine's stream over the timed region)
+  cpu_baseline  libsodium crypto_sign_verify_detached (the function
+                PubKeyUtils::verifySig calls), multithreaded on this host's
+                cores over a bounded sample of the same dataset
+  latency_1k    p50/p99 end-to-end latency of 1000-signature SCP-sized batches
+                through the host API (H2D + kernel + D2H)
+"""
+import argparse
+import ctypes
+import hashlib
+import importlib
+import json
+import os
+import struct
+import sys
+import threading
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "ed25519 verifies/sec @1M batch (1/8 GPU) + p50 latency @1k batch"
+# Algorithmic work per verify: ~1524 field squarings x 44 +
+# ~1488 multiplications x 72 32x32->64 multiply-adds of the 8x32-bit-limb
+# schoolbook formulation of libsodium's op count.
+W_MAD_PER_VERIFY = 174192
+# Measured VALU issue peak of v_mad_u64_u32 on MI355X (profiles/r01_ubench_imul.txt,
+# 8 waves/SIMD, 8 independent chains/lane): 3.485e13 lane-ops/s per GPU.
+PEAK_MAD_PER_S = 3.485e13
+PEAK_SOURCE = "profiles/r01_ubench_imul.txt (v_mad_u64_u32, measured on MI355X)"
+NOMINAL_PEAK_SURVEY = 9.83e12  # SURVEY.md §8 d7 assumption (quarter-rate); measured rate is 3.5x higher
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def seeds_and_msgs(lo, hi):
+    seeds = bytearray()
+    msgs = bytearray()
+    for i in range(lo, hi):
+        p = struct.pack("<Q", i)
+        seeds += hashlib.sha256(b"SVSEED" + p).digest()
+        msgs += hashlib.sha256(b"SVMSG" + p).digest()
+    return np.frombuffer(bytes(seeds), np.uint8), np.frombuffer(bytes(msgs), np.uint8)
+
+
+def load_libsodium():
+    for name in ("libsodium.so.23", "libsodium.so", "/opt/conda/lib/libsodium.so.23"):
+        try:
+            lib = ctypes.CDLL(name)
+            if lib.sodium_init() < 0:
+                continue
+            lib.sodium_version_string.restype = ctypes.c_char_p
+            return lib
+        except OSError:
+            continue
+    return None
+
+
+def cpu_verify_rate(pk, sig, msg, mlen, threads, lib, kind):
+    """Verify rows [0, n) with `threads` Python threads (ctypes drops the GIL)."""
+    n = pk.shape[0]
+    out = np.zeros(n, np.uint8)
+    pkb, sgb, msb = pk.tobytes(), sig.tobytes(), msg.tobytes()
+
+    def work(lo, hi):
+        if kind == "reference":
+            f = lib.crypto_sign_verify_detached
+            for i in range(lo, hi):
+                out[i] = f(sgb[64 * i:64 * i + 64], msb[mlen * i:mlen * i + mlen], ctypes.c_ulonglong(mlen),
+                           pkb[32 * i:32 * i + 32]) == 0
+        else:
+            f = lib.oracle_ed25519_verify
+            for i in range(lo, hi):
+                out[i] = f(sgb[64 * i:64 * i + 64], msb[mlen * i:mlen * i + mlen], ctypes.c_size_t(mlen),
+                           pkb[32 * i:32 * i + 32]) == 0
+
+    th = [threading.Thread(target=work, args=(t * n // threads, (t + 1) * n // threads)) for t in range(threads)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    dt = time.perf_counter() - t0
+    return n / dt, dt, out
+
+
+def scp_latency_set(sodium, n=1000, adversarial=0.1, seed=20250211):
+    """Config 4: 100 validators, 1000 signatures over 128-384 B messages, 10% adversarial."""
+    rng = np.random.default_rng(seed)
+    vals = []
+    for v in range(100):
+        pk = ctypes.create_string_buffer(32)
+        sk = ctypes.create_string_buffer(64)
+        sodium.crypto_sign_seed_keypair(pk, sk, hashlib.sha256(b"SVVAL" + struct.pack("<Q", v)).digest())
+        vals.append((pk.raw, sk.raw))
+    pks, sigs, msgs, expect = [], [], [], []
+    n_adv = int(n * adversarial)
+    adv_rows = set(rng.choice(n, n_adv, replace=False).tolist())
+    L = 2**252 + 27742317777372353535851937790883648493
+    for i in range(n):
+        pk, sk = vals[i % 100]
+        m = rng.integers(0, 256, int(rng.integers(128, 385)), dtype=np.uint8).tobytes()
+        s = ctypes.create_string_buffer(64)
+        sodium.crypto_sign_detached(s, None, m, ctypes.c_ulonglong(len(m)), sk)
+        sig = bytearray(s.raw)
+        pkb = bytearray(pk)
+        if i in adv_rows:
+            kind = i % 5
+            if kind == 0:      # non-canonical S (S + L)
+                S = int.from_bytes(sig[32:], "little") + L
+                sig[32:] = S.to_bytes(32, "little")
+            elif kind == 1:    # small-order R
+                sig[:32] = bytes.fromhex("c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a")
+            elif kind == 2:    # small-order A
+                pkb[:] = bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05")
+            elif kind == 3:    # non-canonical A (y = p)
+                pkb[:] = ((2**255 - 19)).to_bytes(32, "little")
+            else:              # flipped R bit
+                sig[3] ^= 0x10
+        ok = sodium.crypto_sign_verify_detached(bytes(sig), m, ctypes.c_ulonglong(len(m)), bytes(pkb)) == 0
+        pks.append(bytes(pkb)); sigs.append(bytes(sig)); msgs.append(m); expect.append(1 if ok else 0)
+    return pks, sigs, msgs, np.array(expect, np.uint8)
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="signatures per GPU per step")
+    ap.add_argument("--latency-iters", type=int, default=200)
+    ap.add_argument("--cpu-sample", type=int, default=131072)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-latency", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+
+    import torch  # device memory + streams; imported before the engine so both share one HIP runtime
+    import torch.distributed as dist
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    sv = importlib.import_module("stellar-core_amd")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def sync():
+        sv.synchronize(local)
+        torch.cuda.synchronize(dev)
+
+    n = args.batch
+    lo = rank * n
+    t_gen = time.perf_counter()
+    seeds, msgs = seeds_and_msgs(lo, lo + n)
+    d_seed = torch.from_numpy(seeds.copy()).to(dev)
+    d_msg = torch.from_numpy(msgs.copy()).to(dev)
+    d_pk = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    d_sig = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    d_verdict = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    sv.sign_device(local, d_seed.data_ptr(), d_msg.data_ptr(), n, d_pk.data_ptr(), d_sig.data_ptr(), stream)
+    sync()
+    log("rank %d: dataset [%d, %d) generated on device in %.2fs" % (rank, lo, lo + n, time.perf_counter() - t_gen))
+
+    digest_ok = None
+    pk_h = sig_h = None
+    if rank == 0:
+        pk_h = d_pk.cpu().numpy().reshape(n, 32)
+        sig_h = d_sig.cpu().numpy().reshape(n, 64)
+        with open(os.path.join(REPO, "tests", "golden", "digests.json")) as f:
+            want = json.load(f)
+        if str(n) in want:
+            stream_bytes = np.concatenate([pk_h, sig_h, msgs.reshape(n, 32)], axis=1).tobytes()
+            digest_ok = hashlib.sha256(stream_bytes).hexdigest() == want[str(n)]
+            log("dataset digest vs libsodium (%d sigs): %s" % (n, "MATCH" if digest_ok else "MISMATCH"))
+
+    def step():
+        sv.verify_device(local, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), n, d_verdict.data_ptr(),
+                         d_bitmap.data_ptr(), stream)
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    barrier()
+    sv.kernel_time_reset()
+    sv.timing_enable(True)
+    sync()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    sv.timing_enable(False)
+    k_ms, k_launches, k_sigs = sv.kernel_time(local)
+    # every signature of the dataset is valid: all verdict bytes 1 and every
+    # full ballot word of the bitmap all-ones
+    verdict_count = int(d_verdict.sum(dtype=torch.int64).item())
+    full = n // 64
+    bitmap_ok = bool((d_bitmap[:full] == -1).all().item())
+    verdicts_ok = verdict_count == n and bitmap_ok
+
+    if world > 1:
+        t = torch.tensor([elapsed, 0.0 if verdicts_ok else 1.0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, bad = float(t[0]), float(t[1])
+        verdicts_ok = bad == 0.0
+    total = n * world * args.steps
+    value = total / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+    kernel_ms = k_ms / max(1, k_launches)
+    kernel_rate = n / (kernel_ms * 1e-3) if kernel_ms > 0 else 0.0
+
+    result = None
+    if rank == 0:
+        achieved = kernel_rate * W_MAD_PER_VERIFY / 1e12
+        traffic = None
+        tf = os.path.join(REPO, "profiles", "r01_traffic.json")
+        if os.path.exists(tf):
+            try:
+                with open(tf) as f:
+                    tj = json.load(f)
+                if int(tj.get("batch", -1)) == n:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        result = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "verifies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: RFC 8032 keypairs/signatures generated on-device from SHA-256 seeds "
+                    "(digest-checked against libsodium 1.0.18), 32-byte messages",
+            "config": {
+                "workload": "BASELINE config 2: 2^20 uniform random valid ed25519 signatures, one batch per GPU "
+                            "(N GPUs: contiguous index slices of one global dataset)",
+                "batch_per_gpu": n,
+                "global_batch": n * world,
+                "msg_len": 32,
+                "parallelism": "shard%d (contiguous slices, no collective)" % world,
+            },
+            "verdicts_ok": verdicts_ok,
+            "dataset_digest_ok": digest_ok,
+            "kernel": {"ms_per_launch": kernel_ms, "launches": k_launches, "verifies_per_s": kernel_rate},
+            "roofline": {
+                "bound": "valu-int",
+                "achieved": achieved,
+                "peak": PEAK_MAD_PER_S / 1e12,
+                "unit": "T mad32/s",
+                "frac": achieved / (PEAK_MAD_PER_S / 1e12),
+                "traffic": traffic,
+                "algorithmic_per_verify": W_MAD_PER_VERIFY,
+                "peak_source": PEAK_SOURCE,
+                "frac_vs_survey_nominal_peak": kernel_rate * W_MAD_PER_VERIFY / NOMINAL_PEAK_SURVEY,
+            },
+        }
+
+    # ---- latency @1k batch (config 4), rank 0 only
+    sodium = load_libsodium() if rank == 0 else None
+    if rank == 0 and not args.no_latency:
+        if sodium is not None:
+            pks, sigs, lmsgs, expect = scp_latency_set(sodium)
+            src = "SCP-sized 128-384 B messages, 100 validators, 10% adversarial (libsodium-signed, libsodium verdicts)"
+        else:
+            k = 1000
+            pks = [pk_h[i].tobytes() for i in range(k)]
+            sigs = [sig_h[i].tobytes() for i in range(k)]
+            lmsgs = [msgs[32 * i:32 * i + 32].tobytes() for i in range(k)]
+            expect = np.ones(k, np.uint8)
+            src = "first 1000 of the device dataset (32 B messages; libsodium unavailable for SCP-sized set)"
+        pk_a = np.frombuffer(b"".join(pks), np.uint8).reshape(-1, 32)
+        sg_a = np.frombuffer(b"".join(sigs), np.uint8).reshape(-1, 64)
+        for _ in range(5):
+            out = sv.verify_messages(pk_a, sg_a, lmsgs, device=local)
+        lat = []
+        for _ in range(args.latency_iters):
+            t1 = time.perf_counter()
+            out = sv.verify_messages(pk_a, sg_a, lmsgs, device=local)
+            lat.append((time.perf_counter() - t1) * 1e3)
+        lat = np.array(lat)
+        result["latency_1k"] = {
+            "batch": len(pks),
+            "p50_ms": float(np.percentile(lat, 50)),
+            "p99_ms": float(np.percentile(lat, 99)),
+            "iters": args.latency_iters,
+            "path": "host API sv_ed25519_verify_batch (pack + H2D + kernel + D2H)",
+            "set": src,
+            "verdicts_match_libsodium": bool((out == expect).all()),
+        }
+
+    # ---- CPU baseline (rank 0, N=1 only)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+        threads = max(1, min(threads, 64))
+        if sodium is not None:
+            kind, lib = "reference", sodium
+            sample = min(args.cpu_sample, n)
+            st_sample = min(8192, n)
+            desc = "libsodium %s crypto_sign_verify_detached (dlopen), first %d signatures of the bench dataset" % (
+                sodium.sodium_version_string().decode(), sample)
+        else:
+            kind = "port"
+            lib = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+            sample = min(4096, n)
+            st_sample = min(512, n)
+            desc = "oracle/ C restatement (libsodium unavailable), first %d signatures" % sample
+        rate, dt, out = cpu_verify_rate(pk_h[:sample], sig_h[:sample], msgs[:32 * sample], 32, threads, lib, kind)
+        rate1, dt1, out1 = cpu_verify_rate(pk_h[:st_sample], sig_h[:st_sample], msgs[:32 * st_sample], 32, 1, lib,
+                                           kind)
+        result["cpu_baseline"] = {
+            "value": rate,
+            "unit": "verifies/s",
+            "cores": threads,
+            "kind": kind,
+            "sample": desc + " (%.1f s wall on %d threads)" % (dt, threads),
+            "single_thread_value": rate1,
+            "cpu_verdicts_all_valid": bool(out.all() and out1.all()),
+            "gpu_over_cpu": value / rate if rate > 0 else None,
+        }
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

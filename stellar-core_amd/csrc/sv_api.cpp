@@ -60,7 +60,7 @@ struct DevBuf {
   size_t cap = 0;
   int ensure(size_t bytes) {
     if (bytes <= cap) return SV_OK;
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
     const size_t want = std::max<size_t>(bytes, 1 << 16);
@@ -73,7 +73,7 @@ struct DevBuf {
     return SV_OK;
   }
   void release() {
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
   }
@@ -81,6 +81,7 @@ struct DevBuf {
 
 struct Device {
   int id = -1;
+  bool ready = false;  // resources created lazily on first use (under mu)
   int cus = 0;
   unsigned grid = 0;  // persistent grid (workgroups)
   hipStream_t stream = nullptr;
@@ -121,28 +122,29 @@ int init_device(Device& D, int id) {
   return SV_OK;
 }
 
+// Enumerates devices only; per-device resources are created on first use so a
+// process that drives one GPU (one rank per GPU) never touches the others.
 int ensure_init() {
   std::lock_guard<std::mutex> g(g_mu);
   if (g_inited) return g_devs.empty() ? fail(SV_ERR_NO_DEVICE, "no HIP device") : SV_OK;
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
-  if (e != hipSuccess || n <= 0) {
-    g_inited = true;
-    return fail(SV_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
-  }
+  g_inited = true;
+  if (e != hipSuccess || n <= 0) return fail(SV_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
   for (int i = 0; i < n; ++i) {
     Device* D = new Device();
-    int rc = init_device(*D, i);
-    if (rc != SV_OK) {
-      delete D;
-      for (Device* d : g_devs) delete d;
-      g_devs.clear();
-      return rc;
-    }
+    D->id = i;
     g_devs.push_back(D);
   }
-  g_inited = true;
   return SV_OK;
+}
+
+// Caller holds D.mu.
+int ready_locked(Device& D) {
+  if (D.ready) return SV_OK;
+  int rc = init_device(D, D.id);
+  if (rc == SV_OK) D.ready = true;
+  return rc;
 }
 
 unsigned grid_for(const Device& D, uint64_t n) {
@@ -178,8 +180,8 @@ int harvest_timing_locked(Device& D) {
     D.total_ms += ms;
     D.launches += 1;
     D.sigs += D.pending_n[k];
-    hipEventDestroy(D.pending[k].first);
-    hipEventDestroy(D.pending[k].second);
+    (void)hipEventDestroy(D.pending[k].first);
+    (void)hipEventDestroy(D.pending[k].second);
   }
   D.pending.clear();
   D.pending_n.clear();
@@ -193,6 +195,7 @@ int verify_host_slice(Device& D, const uint8_t* pk, const uint8_t* sig, const ui
   std::lock_guard<std::mutex> g(D.mu);
   SV_HIP(hipSetDevice(D.id));
   int rc;
+  if ((rc = ready_locked(D))) return rc;
   if ((rc = D.pk.ensure(n * 32)) || (rc = D.sig.ensure(n * 64)) || (rc = D.verdict.ensure(n))) return rc;
   SV_HIP(hipMemcpyAsync(D.pk.p, pk, n * 32, hipMemcpyHostToDevice, D.stream));
   SV_HIP(hipMemcpyAsync(D.sig.p, sig, n * 64, hipMemcpyHostToDevice, D.stream));
@@ -300,19 +303,20 @@ void sv_shutdown(void) {
   std::lock_guard<std::mutex> g(g_mu);
   for (Device* D : g_devs) {
     std::lock_guard<std::mutex> gd(D->mu);
-    hipSetDevice(D->id);
-    hipStreamSynchronize(D->stream);
+    if (!D->ready) continue;
+    (void)hipSetDevice(D->id);
+    (void)hipStreamSynchronize(D->stream);
     for (auto& pr : D->pending) {
-      hipEventDestroy(pr.first);
-      hipEventDestroy(pr.second);
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
     }
     D->pk.release(); D->sig.release(); D->msg.release();
     D->off.release(); D->len.release(); D->verdict.release();
-    if (D->ws) hipFree(D->ws);
-    if (D->btab) hipFree(D->btab);
-    if (D->dep_in) hipEventDestroy(D->dep_in);
-    if (D->dep_out) hipEventDestroy(D->dep_out);
-    if (D->stream) hipStreamDestroy(D->stream);
+    if (D->ws) (void)hipFree(D->ws);
+    if (D->btab) (void)hipFree(D->btab);
+    if (D->dep_in) (void)hipEventDestroy(D->dep_in);
+    if (D->dep_out) (void)hipEventDestroy(D->dep_out);
+    if (D->stream) (void)hipStreamDestroy(D->stream);
   }
   for (Device* D : g_devs) delete D;
   g_devs.clear();
@@ -368,6 +372,7 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
   Device& D = *g_devs[device];
   std::lock_guard<std::mutex> g(D.mu);
   SV_HIP(hipSetDevice(D.id));
+  if ((rc = ready_locked(D))) return rc;
   hipStream_t user = (hipStream_t)stream;
   SV_HIP(hipEventRecord(D.dep_in, user));
   SV_HIP(hipStreamWaitEvent(D.stream, D.dep_in, 0));
@@ -391,6 +396,7 @@ int sv_ed25519_sign_device(int device, const void* d_seed, const void* d_msg32, 
   Device& D = *g_devs[device];
   std::lock_guard<std::mutex> g(D.mu);
   SV_HIP(hipSetDevice(D.id));
+  if ((rc = ready_locked(D))) return rc;
   hipStream_t user = (hipStream_t)stream;
   SV_HIP(hipEventRecord(D.dep_in, user));
   SV_HIP(hipStreamWaitEvent(D.stream, D.dep_in, 0));
@@ -411,6 +417,12 @@ int sv_kernel_time(int device, double* total_ms, uint64_t* launches, uint64_t* s
   if (device < 0 || device >= (int)g_devs.size()) return fail(SV_ERR_INVALID_ARG, "device index out of range");
   Device& D = *g_devs[device];
   std::lock_guard<std::mutex> g(D.mu);
+  if (!D.ready) {
+    if (total_ms) *total_ms = 0;
+    if (launches) *launches = 0;
+    if (signatures) *signatures = 0;
+    return SV_OK;
+  }
   SV_HIP(hipSetDevice(D.id));
   if ((rc = harvest_timing_locked(D))) return rc;
   if (total_ms) *total_ms = D.total_ms;
@@ -424,7 +436,8 @@ int sv_kernel_time_reset(void) {
   if (rc) return rc;
   for (Device* D : g_devs) {
     std::lock_guard<std::mutex> g(D->mu);
-    hipSetDevice(D->id);
+    if (!D->ready) continue;
+    (void)hipSetDevice(D->id);
     if ((rc = harvest_timing_locked(*D))) return rc;
     D->total_ms = 0;
     D->launches = 0;
@@ -439,6 +452,7 @@ int sv_device_synchronize(int device) {
   if (device < 0 || device >= (int)g_devs.size()) return fail(SV_ERR_INVALID_ARG, "device index out of range");
   Device& D = *g_devs[device];
   std::lock_guard<std::mutex> g(D.mu);
+  if (!D.ready) return SV_OK;
   SV_HIP(hipSetDevice(D.id));
   SV_HIP(hipStreamSynchronize(D.stream));
   return SV_OK;
