@@ -79,32 +79,33 @@ def load_libsodium():
     return None
 
 
-def cpu_verify_rate(pk, sig, msg, mlen, threads, lib, kind):
-    """Verify rows [0, n) with `threads` Python threads (ctypes drops the GIL)."""
+def cpu_verify_rate(pk, sig, msg, mlen, threads, sodium_path):
+    """Native pthread harness (oracle/cpu_baseline.c): libsodium when
+    sodium_path is given ("reference"), else the oracle restatement ("port")."""
+    base = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+    base.cpubase_run.restype = ctypes.c_double
+    base.cpubase_run.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_uint32, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
     n = pk.shape[0]
+    pk = np.ascontiguousarray(pk)
+    sig = np.ascontiguousarray(sig)
+    msg = np.ascontiguousarray(msg)
     out = np.zeros(n, np.uint8)
-    pkb, sgb, msb = pk.tobytes(), sig.tobytes(), msg.tobytes()
-
-    def work(lo, hi):
-        if kind == "reference":
-            f = lib.crypto_sign_verify_detached
-            for i in range(lo, hi):
-                out[i] = f(sgb[64 * i:64 * i + 64], msb[mlen * i:mlen * i + mlen], ctypes.c_ulonglong(mlen),
-                           pkb[32 * i:32 * i + 32]) == 0
-        else:
-            f = lib.oracle_ed25519_verify
-            for i in range(lo, hi):
-                out[i] = f(sgb[64 * i:64 * i + 64], msb[mlen * i:mlen * i + mlen], ctypes.c_size_t(mlen),
-                           pkb[32 * i:32 * i + 32]) == 0
-
-    th = [threading.Thread(target=work, args=(t * n // threads, (t + 1) * n // threads)) for t in range(threads)]
-    t0 = time.perf_counter()
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    dt = time.perf_counter() - t0
+    dt = base.cpubase_run(sodium_path.encode() if sodium_path else None, pk.ctypes.data, sig.ctypes.data,
+                          msg.ctypes.data, mlen, n, threads, out.ctypes.data)
+    if dt <= 0:
+        raise RuntimeError("cpu baseline harness failed (%s)" % dt)
     return n / dt, dt, out
+
+
+def sodium_path():
+    for p in ("/opt/conda/lib/libsodium.so.23", "libsodium.so.23", "libsodium.so"):
+        try:
+            ctypes.CDLL(p)
+            return p
+        except OSError:
+            continue
+    return None
 
 
 def scp_latency_set(sodium, n=1000, adversarial=0.1, seed=20250211):
@@ -152,7 +153,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20, help="signatures per GPU per step")
     ap.add_argument("--latency-iters", type=int, default=200)
-    ap.add_argument("--cpu-sample", type=int, default=131072)
+    ap.add_argument("--cpu-sample", type=int, default=262144)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     args = ap.parse_args()
@@ -334,27 +335,27 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
         threads = max(1, min(threads, 64))
-        if sodium is not None:
-            kind, lib = "reference", sodium
+        spath = sodium_path() if sodium is not None else None
+        if spath is not None:
+            kind = "reference"
             sample = min(args.cpu_sample, n)
-            st_sample = min(8192, n)
-            desc = "libsodium %s crypto_sign_verify_detached (dlopen), first %d signatures of the bench dataset" % (
-                sodium.sodium_version_string().decode(), sample)
+            st_sample = min(16384, n)
+            desc = "libsodium %s crypto_sign_verify_detached (dlopen %s), first %d signatures of the bench dataset" % (
+                sodium.sodium_version_string().decode(), spath, sample)
         else:
             kind = "port"
-            lib = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
-            sample = min(4096, n)
-            st_sample = min(512, n)
+            sample = min(8192, n)
+            st_sample = min(1024, n)
             desc = "oracle/ C restatement (libsodium unavailable), first %d signatures" % sample
-        rate, dt, out = cpu_verify_rate(pk_h[:sample], sig_h[:sample], msgs[:32 * sample], 32, threads, lib, kind)
-        rate1, dt1, out1 = cpu_verify_rate(pk_h[:st_sample], sig_h[:st_sample], msgs[:32 * st_sample], 32, 1, lib,
-                                           kind)
+        rate, dt, out = cpu_verify_rate(pk_h[:sample], sig_h[:sample], msgs[:32 * sample], 32, threads, spath)
+        rate1, dt1, out1 = cpu_verify_rate(pk_h[:st_sample], sig_h[:st_sample], msgs[:32 * st_sample], 32, 1, spath)
         result["cpu_baseline"] = {
             "value": rate,
             "unit": "verifies/s",
             "cores": threads,
             "kind": kind,
-            "sample": desc + " (%.1f s wall on %d threads)" % (dt, threads),
+            "sample": desc + " (%.2f s wall on %d pthreads, static contiguous partition; native harness "
+                             "oracle/cpu_baseline.c)" % (dt, threads),
             "single_thread_value": rate1,
             "cpu_verdicts_all_valid": bool(out.all() and out1.all()),
             "gpu_over_cpu": value / rate if rate > 0 else None,

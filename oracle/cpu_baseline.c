@@ -1,0 +1,69 @@
+/*
+ * CPU BASELINE HARNESS — test/bench infrastructure only (bench.py's
+ * cpu_baseline leg).  Never part of the product path.
+ *
+ * Times the CPU path stellar-core uses today: libsodium
+ * crypto_sign_verify_detached, the call PubKeyUtils::verifySig makes on a cache
+ * miss (/root/reference/src/crypto/SecretKey.cpp:461-463), over n fixed-length
+ * messages on `threads` pthreads with a static contiguous partition (SURVEY.md
+ * §8 d8).  libsodium is dlopen'd from `sodium_path`; with sodium_path == NULL
+ * the oracle restatement (ed25519_oracle.c) is timed instead ("port").
+ */
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <time.h>
+
+#include "oracle.h"
+
+typedef int (*verify_fn)(const unsigned char*, const unsigned char*, unsigned long long, const unsigned char*);
+
+struct job {
+  verify_fn sodium;
+  const uint8_t *pk, *sig, *msg;
+  uint32_t mlen;
+  size_t lo, hi;
+  uint8_t* out;
+};
+
+static void* worker(void* arg) {
+  struct job* j = (struct job*)arg;
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    int rc = j->sodium ? j->sodium(j->sig + 64 * i, j->msg + (size_t)j->mlen * i, j->mlen, j->pk + 32 * i)
+                       : oracle_ed25519_verify(j->sig + 64 * i, j->msg + (size_t)j->mlen * i, j->mlen, j->pk + 32 * i);
+    j->out[i] = rc == 0;
+  }
+  return 0;
+}
+
+/* Returns wall seconds (< 0 on error: -1 dlopen, -2 dlsym/init, -3 threads). */
+double cpubase_run(const char* sodium_path, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t mlen,
+                   size_t n, int threads, uint8_t* out) {
+  verify_fn f = 0;
+  if (sodium_path) {
+    void* h = dlopen(sodium_path, RTLD_NOW | RTLD_LOCAL);
+    if (!h) return -1.0;
+    int (*init)(void) = (int (*)(void))dlsym(h, "sodium_init");
+    f = (verify_fn)dlsym(h, "crypto_sign_verify_detached");
+    if (!init || !f || init() < 0) return -2.0;
+  }
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  struct job jobs[256];
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < threads; ++t) {
+    jobs[t].sodium = f;
+    jobs[t].pk = pk; jobs[t].sig = sig; jobs[t].msg = msg; jobs[t].mlen = mlen;
+    jobs[t].lo = (size_t)t * n / threads;
+    jobs[t].hi = (size_t)(t + 1) * n / threads;
+    jobs[t].out = out;
+    if (pthread_create(&th[t], 0, worker, &jobs[t]) != 0) return -3.0;
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -1,0 +1,74 @@
+"""The C-ABI library builds for gfx950, loads on a CPU-only host and exports
+every entry point include/*.h declares; the product path fails loudly (no CPU
+fallback) when no GPU is present."""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+
+def _declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(REPO, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"\b(sv_[a-z0-9_]+)\s*\(", src):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+@pytest.fixture(scope="module")
+def lib_path(sv):
+    if not os.path.exists(sv.LIB_PATH):
+        subprocess.run(["make", "-s", "-j4"], cwd=os.path.join(REPO, "stellar-core_amd"), check=True)
+    return sv.LIB_PATH
+
+
+def test_header_declares_expected_surface():
+    names = _declared_functions()
+    for must in ["sv_init", "sv_shutdown", "sv_device_count", "sv_last_error_string", "sv_ed25519_verify_batch",
+                 "sv_ed25519_verify_batch_fixed", "sv_ed25519_verify_device", "sv_ed25519_sign_device"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(lib_path, sv):
+    lib = ctypes.CDLL(lib_path)
+    for name in _declared_functions():
+        assert hasattr(lib, name), name
+    assert set(sv.EXPORTED_SYMBOLS) <= set(_declared_functions())
+
+
+def test_code_object_is_gfx950_only(lib_path):
+    blob = open(lib_path, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa-[-a-z]*(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}, targets
+
+
+def test_no_cpu_fallback_without_gpu(sv):
+    """On a host without a GPU every verify entry point raises (never rejects)."""
+    try:
+        n = sv.device_count()
+    except sv.SigVerifyError:
+        n = 0
+    if n > 0:
+        pytest.skip("a GPU is present")
+    d = np.load(os.path.join(REPO, "tests", "golden", "intree.npz"))
+    with pytest.raises(sv.SigVerifyError):
+        sv.verify_batch(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"])
+    with pytest.raises(sv.SigVerifyError):
+        sv.verify_fixed(d["pk"][:2], d["sig"][:2], np.zeros(64, np.uint8))
+
+
+def test_python_binding_validates_shapes(sv):
+    with pytest.raises(ValueError):
+        sv.verify_batch(np.zeros((2, 32), np.uint8), np.zeros((3, 64), np.uint8), np.zeros(4, np.uint8),
+                        [0, 0], [1, 1])
+    with pytest.raises(ValueError):
+        sv.verify_batch(np.zeros((2, 32), np.uint8), np.zeros((2, 64), np.uint8), np.zeros(4, np.uint8),
+                        [0, 3], [1, 2])

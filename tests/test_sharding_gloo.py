@@ -1,0 +1,79 @@
+"""N>1 path on CPU: world_size-2 gloo ranks shard one batch into contiguous
+slices (stellar-core_amd/sharding.py, the partition bench.py and the C-ABI
+use), verify their slice with the oracle as a stand-in for the GPU, gather the
+verdict bytes and must reproduce the single-process verdicts and digest."""
+import importlib
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO, load_golden
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, rows, q):
+    sys.path.insert(0, REPO)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ctypes
+    sh = importlib.import_module("stellar-core_amd.sharding")
+    oracle = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+    d = load_golden("adversarial")
+    n = len(rows)
+    lo, hi = sh.shard_bounds(n, world, rank)
+    local = []
+    for i in rows[lo:hi]:
+        o, ln = int(d["msg_off"][i]), int(d["msg_len"][i])
+        ok = oracle.oracle_ed25519_verify(d["sig"][i].tobytes(), d["msg"][o:o + ln].tobytes(),
+                                          ctypes.c_size_t(ln), d["pk"][i].tobytes()) == 0
+        local.append(1 if ok else 0)
+    full = sh.gather_verdicts(np.array(local, np.uint8), n, world, rank)
+    if rank == 0:
+        q.put((full.tolist(), sh.verdict_digest(full)))
+    dist.destroy_process_group()
+
+
+def test_shard_bounds_partition():
+    sh = importlib.import_module("stellar-core_amd.sharding")
+    for n in [0, 1, 7, 64, 1000, 1 << 20]:
+        for world in [1, 2, 3, 8]:
+            b = [sh.shard_bounds(n, world, r) for r in range(world)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[r][1] == b[r + 1][0] for r in range(world - 1))
+            assert max(h - lo for lo, h in b) - min(h - lo for lo, h in b) <= 1
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_world2_gather_matches_single_process(world):
+    d = load_golden("adversarial")
+    rng = np.random.default_rng(0)
+    rows = np.sort(rng.choice(len(d["verdict"]), 61, replace=False))  # odd size: ragged shards
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, rows, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full, digest = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sh = importlib.import_module("stellar-core_amd.sharding")
+    want = d["verdict"][rows]
+    assert np.array_equal(np.array(full, np.uint8), want)
+    assert digest == sh.verdict_digest(want)
