@@ -7,9 +7,11 @@
 // ballot word of the verdict bitmap per wave iteration).
 //
 // Memory per workgroup: the 129-entry base-point table (18.6 KiB) in LDS.
-// Memory per lane: a 1440 B slot of the HBM workspace for the signature's
-// 9-entry table of multiples of -A, interleaved so that quad q of entry e of
-// the 64 lanes of a wave is one contiguous 1 KiB line.
+// Memory per lane: a 1728 B slot of the HBM workspace for the signature's
+// 9-entry table of multiples of -A, lane-major: lanes gather different
+// entries (per-lane digits), so keeping each lane's entry contiguous (192 B)
+// is what bounds the line traffic (a wave-interleaved layout measured ~8x
+// line amplification, profiles/r01_*).
 #include <hip/hip_runtime.h>
 
 #include "verify_core.h"
@@ -27,7 +29,7 @@ struct sv_kparams {
   uint32_t fixed_len;     // 0 = variable-length
   uint8_t* verdict;       // n bytes
   uint64_t* bitmap;       // optional, ceil(n/64) words
-  sv_u4* ws;              // workspace: (grid threads / 64) x 9 x 10 x 64 quads
+  sv_u4* ws;              // workspace: grid threads x 9 entries x 12 quads (lane-major)
   const sv_u4* btab;      // SV_BTAB_ENTRIES x 9 quads (global copy)
 };
 
@@ -49,8 +51,8 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_kernel(
 
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t wave = gtid >> 6;
-  sv_u4* slot = p.ws + wave * (SV_ATAB_ENTRIES * SV_ATAB_QUADS * 64) + lane;
+  // lane-major workspace slot: this lane's 9 table entries, 1728 contiguous bytes
+  sv_u4* slot = p.ws + gtid * (SV_ATAB_ENTRIES * SV_ATAB_QUADS);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
 
   for (uint64_t base = gtid - lane; base < p.n; base += stride) {
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_kernel(
     } else {
       sha512_ram_var(hram, R, A, p.msg + ii * (uint64_t)p.fixed_len, p.fixed_len);
     }
-    const bool ok = sv_verify_core(A, p.sig + 4 * ii, S, hram, slot, 64, s_btab) && active;
+    const bool ok = sv_verify_core(A, p.sig + 4 * ii, S, hram, slot, 1, s_btab) && active;
     if (active) p.verdict[i] = ok ? 1 : 0;
     const uint64_t mask = __ballot(ok);
     if (p.bitmap != nullptr && lane == 0) p.bitmap[base >> 6] = mask;
@@ -97,7 +99,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_sign_kernel(sv
   sv_load_btab_lds(s_btab, p.btab);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  sv_u4* slot = p.ws + (gtid >> 6) * (SV_ATAB_ENTRIES * SV_ATAB_QUADS * 64) + lane;
+  sv_u4* slot = p.ws + gtid * (SV_ATAB_ENTRIES * SV_ATAB_QUADS);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = gtid - lane; base < p.n; base += stride) {
     const uint64_t i = base + lane;
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_sign_kernel(sv
     uint32_t seed[8], M[8], pk[8], sig[16];
     sv_unpack2(seed, p.seed + 2 * ii);
     sv_unpack2(M, p.msg + 2 * ii);
-    sv_sign_lane(pk, sig, seed, M, slot, 64, s_btab);
+    sv_sign_lane(pk, sig, seed, M, slot, 1, s_btab);
     if (active) {
       p.pk[2 * i] = sv_u4{pk[0], pk[1], pk[2], pk[3]};
       p.pk[2 * i + 1] = sv_u4{pk[4], pk[5], pk[6], pk[7]};

@@ -17,7 +17,8 @@
 //   d_A in [-8, 7] (signed radix 16 of h); on even windows also add
 //   table_B[d_B], d_B in [-128, 127] (signed radix 256 of S).
 //   table_A = {0..8}·(-A) in cached form, built per lane into an HBM workspace
-//   slot (1440 B/lane, too big for LDS at >=2 waves/SIMD);
+//   slot (1728 B/lane, lane-major so a lane's entry is 192 contiguous bytes;
+//   too big for LDS at >= 2 waves/SIMD);
 //   table_B = {0..128}·B in affine precomp form, shared by the workgroup in LDS.
 //   Zero digits add the identity entry, so every lane does identical work.
 #pragma once
@@ -126,6 +127,8 @@ SV_HD void sv_double_scalarmult_encode(uint32_t enc[8], const ge_p3& negA, const
       if (s < 4) {
         ge_dbl(Q, P.X, P.Y, P.Z);
       } else {
+        // (loading the table_A entry earlier, before the doublings, spills:
+        // a doubling leaves no room for 40 more live VGPRs at 2 waves/SIMD)
         fe qa, qb, qz, qt;
         bool neg;
         if (s == 4) {

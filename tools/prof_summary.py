@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 profile directory of bench.py runs (developer tool).
+
+Reads <dir>/kt/*_kernel_stats.csv and every <dir>/*/*_counter_collection.csv,
+averages each counter over the sv_verify_kernel<0> dispatches and prints a
+JSON summary with per-launch HBM traffic (FETCH_SIZE doubled per
+MI355X_MICROARCH.md §HBM for 16-B streaming reads is NOT applied here: our
+reads are 16-B per-lane gathers, so both the raw and the doubled value are
+reported), VALU instruction counts per signature and issue efficiency.
+
+Usage: python tools/prof_summary.py gpurun_out/prof2 [--batch 1048576]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main():
+    d = sys.argv[1]
+    batch = 1 << 20
+    if "--batch" in sys.argv:
+        batch = int(sys.argv[sys.argv.index("--batch") + 1])
+    out = {"profile_dir": d, "batch": batch}
+    ks = glob.glob(os.path.join(d, "kt", "*_kernel_stats.csv"))
+    if ks:
+        for r in csv.DictReader(open(ks[0])):
+            if "sv_verify_kernel" in r["Name"]:
+                out["kernel"] = r["Name"]
+                out["calls"] = int(r["Calls"])
+                out["avg_ns"] = float(r["AverageNs"])
+                out["min_ns"] = float(r["MinNs"])
+                out["max_ns"] = float(r["MaxNs"])
+    vals = defaultdict(list)
+    meta = {}
+    for f in glob.glob(os.path.join(d, "*", "*_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if "sv_verify_kernel<0>" not in r["Kernel_Name"]:
+                continue
+            if int(r["Grid_Size"]) < 1024:
+                continue
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
+                                      "Accum_VGPR_Count", "SGPR_Count")}
+    avg = {k: sum(v) / len(v) for k, v in vals.items()}
+    out["dispatch"] = meta
+    out["counters_avg_per_launch"] = avg
+    if "FETCH_SIZE" in avg:
+        out["fetch_bytes_per_launch_raw"] = avg["FETCH_SIZE"] * 1024
+        out["fetch_bytes_per_launch_x2"] = avg["FETCH_SIZE"] * 1024 * 2
+    if "WRITE_SIZE" in avg:
+        out["write_bytes_per_launch"] = avg["WRITE_SIZE"] * 1024
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        out["hbm_bytes_per_launch"] = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+        out["hbm_bytes_per_verify"] = out["hbm_bytes_per_launch"] / batch
+        out["algorithmic_bytes_per_verify"] = 32 + 64 + 32 + 1
+    if "SQ_INSTS_VALU" in avg:
+        # SQ_INSTS_* count wave-instructions
+        out["valu_inst_per_verify"] = avg["SQ_INSTS_VALU"] * 64 / batch
+        for k in ("SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS",
+                  "SQ_INSTS_SMEM"):
+            if k in avg:
+                out[k.lower() + "_per_verify"] = avg[k] * 64 / batch
+    if "avg_ns" in out and "SQ_INSTS_VALU" in avg:
+        t = out["avg_ns"] * 1e-9
+        out["valu_lane_inst_per_s"] = avg["SQ_INSTS_VALU"] * 64 / t
+    if "GRBM_GUI_ACTIVE" in avg and "avg_ns" in out:
+        out["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / (out["avg_ns"])
+    if "SQ_ACTIVE_INST_VALU" in avg and "SQ_WAVE_CYCLES" in avg:
+        out["valu_active_frac_of_wave_cycles"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
+    if "SQ_BUSY_CYCLES" in avg and "SQ_ACTIVE_INST_VALU" in avg:
+        out["note"] = "SQ_* cycle counters are in quad-cycles (MI355X_MICROARCH.md)"
+    if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
+        out["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
