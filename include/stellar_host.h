@@ -1,0 +1,78 @@
+/*
+ * stellar_host.h — C surface of libstellar_host.so, the C++ mirror of
+ * stellar-core's verification callers re-targeted at the MI355X engine
+ * (stellar-core_amd/csrc/host/).  C++ integrators use the C++ headers
+ * (PubKeyUtils.h, SignatureChecker.h) directly; this surface exists for
+ * bindings and tests.
+ *
+ *   svh_verify_sig          == PubKeyUtils::verifySig
+ *                              (/root/reference/src/crypto/SecretKey.cpp:435-468)
+ *   svh_verify_sig_batch    == PubKeyUtils::verifySigBatch (new)
+ *   svh_cache_*             == clearVerifySigCache / maybeSeedVerifySigCache /
+ *                              flushVerifySigCacheCounts (SecretKey.cpp:317-339)
+ *   svh_check_txset         == SignatureChecker::checkSignature +
+ *                              checkAllSignaturesUsed per tx
+ *                              (/root/reference/src/transactions/SignatureChecker.cpp:30-158),
+ *                              optionally after one GPU batch pre-pass over the
+ *                              whole set
+ */
+#ifndef STELLAR_HOST_H
+#define STELLAR_HOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVH_OK 0
+#define SVH_ERR_INVALID_ARG (-1)
+#define SVH_ERR_ENGINE (-2) /* device error: the batch is unverified, never rejected */
+
+typedef struct svh_signer {
+  uint8_t type; /* 0 ED25519, 1 PRE_AUTH_TX, 2 HASH_X, 3 ED25519_SIGNED_PAYLOAD */
+  uint8_t key[32];
+  uint32_t weight;
+  uint32_t payload_len; /* signed payload only, <= 64 */
+  uint8_t payload[64];
+} svh_signer;
+
+typedef struct svh_decorated_sig {
+  uint8_t hint[4];
+  uint32_t sig_len; /* <= 64; != 64 never verifies */
+  uint8_t sig[64];
+} svh_decorated_sig;
+
+typedef struct svh_tx {
+  uint8_t contents_hash[32];
+  uint32_t protocol;
+  int32_t needed_weight;
+  uint32_t nsigs, sig_off;       /* range in the svh_decorated_sig array */
+  uint32_t nsigners, signer_off; /* range in the svh_signer array */
+} svh_tx;
+
+typedef int (*svh_batch_verify_fn)(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                                   const uint32_t* len, size_t n, uint8_t* verdict);
+
+const char* svh_last_error_string(void);
+void svh_blake2b256(uint8_t out[32], const uint8_t* p, size_t n);
+void svh_sha256(uint8_t out[32], const uint8_t* p, size_t n);
+/* 1 valid, 0 invalid, < 0 error */
+int svh_verify_sig(const uint8_t pk[32], const uint8_t* sig, size_t sig_len, const uint8_t* msg, size_t msg_len);
+int svh_verify_sig_batch(const uint8_t* pk, const uint8_t* sig /* n x 64 */, const uint32_t* sig_len /* NULL = 64 */,
+                         const uint8_t* msg, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
+                         uint8_t* verdict);
+void svh_cache_clear(void);
+void svh_cache_seed(unsigned int seed);
+void svh_cache_counts(uint64_t* hits, uint64_t* misses); /* flushes, like flushVerifySigCacheCounts */
+void svh_engine_counts(uint64_t* signatures, uint64_t* batches);
+/* test hook: route cache misses to fn instead of the GPU (NULL restores) */
+void svh_set_test_verifier(svh_batch_verify_fn fn);
+int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
+                    int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STELLAR_HOST_H */

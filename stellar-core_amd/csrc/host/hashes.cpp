@@ -1,0 +1,161 @@
+// BLAKE2b-256 (RFC 7693) and SHA-256 (FIPS 180-4), written from the specs.
+// Checked against Python hashlib in tests/test_host_mirror.py.
+#include "hashes.h"
+
+#include <cstring>
+
+namespace stellar {
+namespace hostcrypto {
+
+namespace {
+
+// RFC 7693 §2.6: IV = SHA-512 initial values
+const uint64_t kIV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                         0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                         0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+// RFC 7693 §2.7 message schedule SIGMA
+const uint8_t kSigma[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+inline uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+inline uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+inline uint64_t load64le(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+  return v;
+}
+
+}  // namespace
+
+Blake2b256::Blake2b256() : t_{0, 0}, fill_(0) {
+  for (int i = 0; i < 8; ++i) h_[i] = kIV[i];
+  h_[0] ^= 0x01010000ULL ^ 32u;  // depth 1, fanout 1, no key, digest length 32
+  std::memset(buf_, 0, sizeof buf_);
+}
+
+void Blake2b256::compress(bool last) {
+  uint64_t v[16], m[16];
+  for (int i = 0; i < 16; ++i) m[i] = load64le(buf_ + 8 * i);
+  for (int i = 0; i < 8; ++i) {
+    v[i] = h_[i];
+    v[i + 8] = kIV[i];
+  }
+  v[12] ^= t_[0];
+  v[13] ^= t_[1];
+  if (last) v[14] = ~v[14];
+  auto G = [&](int a, int b, int c, int d, uint64_t x, uint64_t y) {
+    v[a] = v[a] + v[b] + x;
+    v[d] = rotr64(v[d] ^ v[a], 32);
+    v[c] = v[c] + v[d];
+    v[b] = rotr64(v[b] ^ v[c], 24);
+    v[a] = v[a] + v[b] + y;
+    v[d] = rotr64(v[d] ^ v[a], 16);
+    v[c] = v[c] + v[d];
+    v[b] = rotr64(v[b] ^ v[c], 63);
+  };
+  for (int r = 0; r < 12; ++r) {
+    const uint8_t* s = kSigma[r];
+    G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+    G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+    G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+    G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+    G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+    G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+    G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+    G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+  }
+  for (int i = 0; i < 8; ++i) h_[i] ^= v[i] ^ v[i + 8];
+}
+
+void Blake2b256::add(const uint8_t* p, size_t n) {
+  while (n > 0) {
+    if (fill_ == 128) {  // only compress when more input follows (last block is special)
+      t_[0] += 128;
+      if (t_[0] < 128) ++t_[1];
+      compress(false);
+      fill_ = 0;
+    }
+    size_t take = 128 - fill_;
+    if (take > n) take = n;
+    std::memcpy(buf_ + fill_, p, take);
+    fill_ += take;
+    p += take;
+    n -= take;
+  }
+}
+
+Hash32 Blake2b256::finish() {
+  t_[0] += fill_;
+  if (t_[0] < fill_) ++t_[1];
+  std::memset(buf_ + fill_, 0, 128 - fill_);
+  compress(true);
+  Hash32 out;
+  for (int i = 0; i < 32; ++i) out[i] = (uint8_t)(h_[i / 8] >> (8 * (i % 8)));
+  return out;
+}
+
+Hash32 blake2b256(const uint8_t* p, size_t n) {
+  Blake2b256 b;
+  b.add(p, n);
+  return b.finish();
+}
+
+Hash32 sha256(const uint8_t* p, size_t n) {
+  static const uint32_t K[64] = {
+      0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+      0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+      0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+      0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+      0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+      0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+      0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+      0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  const uint64_t bits = (uint64_t)n * 8;
+  const size_t total = ((n + 9 + 63) / 64) * 64;
+  uint8_t blk[64];
+  for (size_t off = 0; off < total; off += 64) {
+    for (int i = 0; i < 64; ++i) {
+      const size_t k = off + i;
+      uint8_t b;
+      if (k < n) b = p[k];
+      else if (k == n) b = 0x80;
+      else if (k >= total - 8) b = (uint8_t)(bits >> (8 * (total - 1 - k)));
+      else b = 0;
+      blk[i] = b;
+    }
+    uint32_t w[64];
+    for (int t = 0; t < 16; ++t)
+      w[t] = ((uint32_t)blk[4 * t] << 24) | ((uint32_t)blk[4 * t + 1] << 16) | ((uint32_t)blk[4 * t + 2] << 8) |
+             blk[4 * t + 3];
+    for (int t = 16; t < 64; ++t) {
+      const uint32_t s0 = rotr32(w[t - 15], 7) ^ rotr32(w[t - 15], 18) ^ (w[t - 15] >> 3);
+      const uint32_t s1 = rotr32(w[t - 2], 17) ^ rotr32(w[t - 2], 19) ^ (w[t - 2] >> 10);
+      w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+    }
+    uint32_t a = h[0], b2 = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+    for (int t = 0; t < 64; ++t) {
+      const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+      const uint32_t ch = (e & f) ^ (~e & g);
+      const uint32_t t1 = hh + S1 + ch + K[t] + w[t];
+      const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+      const uint32_t mj = (a & b2) ^ (a & c) ^ (b2 & c);
+      const uint32_t t2 = S0 + mj;
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b2; b2 = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b2; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  }
+  Hash32 out;
+  for (int i = 0; i < 8; ++i)
+    for (int k = 0; k < 4; ++k) out[4 * i + k] = (uint8_t)(h[i] >> (24 - 8 * k));
+  return out;
+}
+
+}  // namespace hostcrypto
+}  // namespace stellar

@@ -1,0 +1,130 @@
+// extern "C" surface of libstellar_host.so (the C++ PubKeyUtils /
+// SignatureChecker mirror), for bindings and tests.  Declared in
+// include/stellar_host.h.  C++ exceptions never cross this boundary.
+#include <cstring>
+#include <exception>
+#include <string>
+#include <vector>
+
+#include "../../../include/stellar_host.h"
+#include "PubKeyUtils.h"
+#include "SignatureChecker.h"
+#include "hashes.h"
+
+using namespace stellar;
+
+namespace {
+thread_local std::string t_err;
+int guard_exc(std::exception const& e) {
+  t_err = e.what();
+  return dynamic_cast<VerifyEngineError const*>(&e) ? SVH_ERR_ENGINE : SVH_ERR_INVALID_ARG;
+}
+}  // namespace
+
+extern "C" {
+
+const char* svh_last_error_string(void) { return t_err.c_str(); }
+
+void svh_blake2b256(uint8_t out[32], const uint8_t* p, size_t n) {
+  auto h = hostcrypto::blake2b256(p, n);
+  std::memcpy(out, h.data(), 32);
+}
+
+void svh_sha256(uint8_t out[32], const uint8_t* p, size_t n) {
+  auto h = hostcrypto::sha256(p, n);
+  std::memcpy(out, h.data(), 32);
+}
+
+int svh_verify_sig(const uint8_t pk[32], const uint8_t* sig, size_t sig_len, const uint8_t* msg, size_t msg_len) {
+  try {
+    PublicKey k;
+    std::memcpy(k.ed25519().data(), pk, 32);
+    Signature s(sig, sig + sig_len);
+    return PubKeyUtils::verifySig(k, s, ByteSlice(msg, msg_len)) ? 1 : 0;
+  } catch (std::exception const& e) {
+    return guard_exc(e);
+  }
+}
+
+int svh_verify_sig_batch(const uint8_t* pk, const uint8_t* sig, const uint32_t* sig_len, const uint8_t* msg,
+                         const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* verdict) {
+  try {
+    std::vector<PublicKey> keys(n);
+    std::vector<Signature> sigs(n);
+    std::vector<PubKeyUtils::VerifyItem> items(n);
+    for (size_t i = 0; i < n; ++i) {
+      std::memcpy(keys[i].ed25519().data(), pk + 32 * i, 32);
+      const uint32_t sl = sig_len ? sig_len[i] : 64;
+      if (sl > 64) throw std::invalid_argument("signature longer than 64 bytes");
+      sigs[i].assign(sig + 64 * i, sig + 64 * i + sl);
+      items[i] = PubKeyUtils::VerifyItem{&keys[i], &sigs[i], ByteSlice(msg + msg_off[i], msg_len[i])};
+    }
+    auto v = PubKeyUtils::verifySigBatch(items);
+    for (size_t i = 0; i < n; ++i) verdict[i] = v[i] ? 1 : 0;
+    return SVH_OK;
+  } catch (std::exception const& e) {
+    return guard_exc(e);
+  }
+}
+
+void svh_cache_clear(void) { PubKeyUtils::clearVerifySigCache(); }
+void svh_cache_seed(unsigned int seed) { PubKeyUtils::maybeSeedVerifySigCache(seed); }
+void svh_cache_counts(uint64_t* hits, uint64_t* misses) {
+  uint64_t h, m;
+  PubKeyUtils::flushVerifySigCacheCounts(h, m);
+  if (hits) *hits = h;
+  if (misses) *misses = m;
+}
+void svh_engine_counts(uint64_t* sigs, uint64_t* batches) {
+  uint64_t s, b;
+  PubKeyUtils::flushEngineCounts(s, b);
+  if (sigs) *sigs = s;
+  if (batches) *batches = b;
+}
+void svh_set_test_verifier(svh_batch_verify_fn fn) { PubKeyUtils::setBatchVerifierForTesting(fn); }
+
+int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
+                    int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs) {
+  try {
+    std::vector<Hash> hashes(ntx);
+    std::vector<std::vector<DecoratedSignature>> dsigs(ntx);
+    std::vector<std::vector<Signer>> sgn(ntx);
+    for (size_t t = 0; t < ntx; ++t) {
+      std::memcpy(hashes[t].data(), txs[t].contents_hash, 32);
+      for (uint32_t k = 0; k < txs[t].nsigs; ++k) {
+        const svh_decorated_sig& s = sigs[txs[t].sig_off + k];
+        if (s.sig_len > 64) throw std::invalid_argument("signature longer than 64 bytes");
+        DecoratedSignature d;
+        std::memcpy(d.hint.data(), s.hint, 4);
+        d.signature.assign(s.sig, s.sig + s.sig_len);
+        dsigs[t].push_back(std::move(d));
+      }
+      for (uint32_t k = 0; k < txs[t].nsigners; ++k) {
+        const svh_signer& s = signers[txs[t].signer_off + k];
+        if (s.type > 3 || s.payload_len > 64) throw std::invalid_argument("bad signer");
+        Signer g;
+        g.key.type = (SignerKeyType)s.type;
+        std::memcpy(g.key.key.data(), s.key, 32);
+        g.key.payload.assign(s.payload, s.payload + s.payload_len);
+        g.weight = s.weight;
+        sgn[t].push_back(std::move(g));
+      }
+    }
+    SignatureBatchPrefetch pre;
+    if (use_prefetch) {
+      for (size_t t = 0; t < ntx; ++t) pre.add(hashes[t], dsigs[t], sgn[t]);
+      pre.run();
+    }
+    if (prefetched_pairs) *prefetched_pairs = pre.pairs();
+    for (size_t t = 0; t < ntx; ++t) {
+      SignatureChecker c(txs[t].protocol, hashes[t], dsigs[t], use_prefetch ? &pre : nullptr);
+      ok[t] = c.checkSignature(sgn[t], txs[t].needed_weight) ? 1 : 0;
+      all_used[t] = c.checkAllSignaturesUsed() ? 1 : 0;
+    }
+    return SVH_OK;
+  } catch (std::exception const& e) {
+    return guard_exc(e);
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,211 @@
+"""C++ host mirror of the reference's verification callers (libstellar_host.so).
+
+CPU tests: the engine is replaced by the oracle through the library's test
+hook (svh_set_test_verifier, the analogue of the reference's BUILD_TESTS
+doubles, SignatureChecker.h:41-63), so the cache / size-64 / counter
+semantics of PubKeyUtils::verifySig (SecretKey.cpp:435-468) and the greedy
+SignatureChecker logic (SignatureChecker.cpp:30-158) are checked without a GPU.
+The GPU variants at the bottom run the same checks through the real engine.
+"""
+import ctypes
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import txset_gen as tg
+from conftest import REPO
+
+VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+
+
+@pytest.fixture(scope="module")
+def host(sv):
+    path = sv.HOSTLIB_PATH
+    if not os.path.exists(path):
+        subprocess.run(["make", "-s", "-j4"], cwd=os.path.join(REPO, "stellar-core_amd"), check=True)
+    lib = ctypes.CDLL(path)
+    lib.svh_verify_sig.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                   ctypes.c_size_t]
+    lib.svh_last_error_string.restype = ctypes.c_char_p
+    lib.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+    return lib
+
+
+class OracleEngine:
+    """Batch verifier callback backed by the oracle; counts calls."""
+
+    def __init__(self, oracle):
+        self.oracle = oracle
+        self.calls = 0
+        self.sigs = 0
+
+        def fn(pk, sig, msg, off, ln, n, out):
+            self.calls += 1
+            self.sigs += n
+            pkb = ctypes.string_at(pk, 32 * n)
+            sgb = ctypes.string_at(sig, 64 * n)
+            offs = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (n,))
+            lens = np.ctypeslib.as_array(ctypes.cast(ln, ctypes.POINTER(ctypes.c_uint32)), (n,))
+            res = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), (n,))
+            for i in range(n):
+                m = ctypes.string_at(msg + int(offs[i]), int(lens[i])) if lens[i] else b""
+                res[i] = 1 if oracle.oracle_ed25519_verify(sgb[64 * i:64 * i + 64], m, len(m),
+                                                           pkb[32 * i:32 * i + 32]) == 0 else 0
+            return 0
+
+        self.cfn = VERIFY_FN(fn)
+
+
+@pytest.fixture()
+def engine(host, oracle):
+    e = OracleEngine(oracle)
+    host.svh_set_test_verifier(ctypes.cast(e.cfn, ctypes.c_void_p))
+    host.svh_cache_clear()
+    host.svh_cache_counts(None, None)
+    host.svh_engine_counts(None, None)
+    yield e
+    host.svh_set_test_verifier(None)
+    host.svh_cache_clear()
+
+
+def _counts(host):
+    h, m = ctypes.c_uint64(), ctypes.c_uint64()
+    host.svh_cache_counts(ctypes.byref(h), ctypes.byref(m))
+    return h.value, m.value
+
+
+def test_blake2b256_and_sha256_match_hashlib(host):
+    out = ctypes.create_string_buffer(32)
+    rng = np.random.default_rng(3)
+    for n in [0, 1, 3, 64, 127, 128, 129, 255, 256, 257, 1000]:
+        b = rng.bytes(n)
+        host.svh_blake2b256(out, b, ctypes.c_size_t(n))
+        assert out.raw == hashlib.blake2b(b, digest_size=32).digest(), n
+        host.svh_sha256(out, b, ctypes.c_size_t(n))
+        assert out.raw == hashlib.sha256(b).digest(), n
+
+
+def test_verify_sig_cache_semantics(host, engine, golden):
+    d = golden["valid"]
+    pk, sig = d["pk"][0].tobytes(), d["sig"][0].tobytes()
+    o, ln = int(d["msg_off"][0]), int(d["msg_len"][0])
+    m = d["msg"][o:o + ln].tobytes()
+    assert host.svh_verify_sig(pk, sig, 64, m, len(m)) == 1       # miss -> engine
+    assert host.svh_verify_sig(pk, sig, 64, m, len(m)) == 1       # hit
+    bad = bytearray(sig)
+    bad[4] ^= 1                                                   # CryptoTests.cpp:292-296
+    assert host.svh_verify_sig(pk, bytes(bad), 64, m, len(m)) == 0
+    assert host.svh_verify_sig(pk, bytes(bad), 64, m, len(m)) == 0  # false verdicts are cached too
+    assert host.svh_verify_sig(pk, sig, 64, m + b"o", len(m) + 1) == 0  # wrong message
+    assert _counts(host) == (2, 3)
+    assert engine.sigs == 3
+    # size != 64: rejected before the cache and the engine (SecretKey.cpp:441-444)
+    assert host.svh_verify_sig(pk, sig, 63, m, len(m)) == 0
+    assert _counts(host) == (0, 0) and engine.sigs == 3
+    host.svh_cache_clear()
+    assert host.svh_verify_sig(pk, sig, 64, m, len(m)) == 1
+    assert _counts(host) == (0, 1)
+
+
+def test_verify_sig_batch_dedup_and_verdicts(host, engine, golden):
+    d = golden["adversarial"]
+    rows = np.arange(0, len(d["verdict"]), 11)
+    rows = np.concatenate([rows, rows[:20]])  # duplicates inside one batch
+    n = len(rows)
+    pk = np.ascontiguousarray(d["pk"][rows])
+    sig = np.ascontiguousarray(d["sig"][rows])
+    off = np.ascontiguousarray(d["msg_off"][rows])
+    ln = np.ascontiguousarray(d["msg_len"][rows])
+    msg = np.ascontiguousarray(d["msg"])
+    out = np.zeros(n, np.uint8)
+    rc = host.svh_verify_sig_batch(pk.ctypes.data_as(ctypes.c_void_p), sig.ctypes.data_as(ctypes.c_void_p), None,
+                                   msg.ctypes.data_as(ctypes.c_void_p), off.ctypes.data_as(ctypes.c_void_p),
+                                   ln.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n),
+                                   out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0
+    assert (out == d["verdict"][rows]).all()
+    assert engine.calls == 1 and engine.sigs == n - 20
+    assert _counts(host) == (20, n - 20)
+
+
+def _oracle_sign_fn(oracle):
+    def sign(reqs):
+        out = []
+        for seed, msg in reqs:
+            pk = ctypes.create_string_buffer(32)
+            sk = ctypes.create_string_buffer(64)
+            oracle.oracle_ed25519_seed_keypair(pk, sk, seed)
+            s = ctypes.create_string_buffer(64)
+            oracle.oracle_ed25519_sign(s, msg, len(msg), sk.raw)
+            out.append((pk.raw, s.raw))
+        return out
+    return sign
+
+
+def _check(host, txs, prefetch):
+    T, S, G = tg.to_ctypes(txs)
+    ok = np.zeros(len(txs), np.uint8)
+    used = np.zeros(len(txs), np.uint8)
+    pairs = ctypes.c_uint64()
+    rc = host.svh_check_txset(T, ctypes.c_size_t(len(txs)), S, G, prefetch, ok.ctypes.data_as(ctypes.c_void_p),
+                              used.ctypes.data_as(ctypes.c_void_p), ctypes.byref(pairs))
+    assert rc == 0, host.svh_last_error_string()
+    return ok, used, pairs.value
+
+
+def test_signature_checker_matches_python_replay(host, engine, oracle):
+    sign = _oracle_sign_fn(oracle)
+    txs = tg.generate(60, sign, seed=11)
+    tg.add_payload_signatures(txs, sign)
+
+    def verify(pk, sig, msg):
+        return oracle.oracle_ed25519_verify(sig, msg, len(msg), pk) == 0
+
+    want_ok, want_used = tg.replay(txs, verify)
+    ok0, used0, _ = _check(host, txs, 0)
+    host.svh_cache_clear()
+    calls_before = engine.calls
+    ok1, used1, pairs = _check(host, txs, 1)
+    assert (ok0 == want_ok).all() and (used0 == want_used).all()
+    assert (ok1 == want_ok).all() and (used1 == want_used).all()
+    assert engine.calls - calls_before == 1  # the whole set went out as ONE batch
+    assert pairs > 0
+    assert 0 < want_ok.sum() < len(txs) or want_ok.sum() == len(txs)
+
+
+@pytest.mark.gpu
+def test_gpu_host_mirror_verify_sig(host, sv, golden):
+    if sv.device_count() < 1:
+        pytest.skip("no GPU")
+    host.svh_set_test_verifier(None)
+    host.svh_cache_clear()
+    d = golden["intree"]
+    for i in range(len(d["verdict"])):
+        o, ln = int(d["msg_off"][i]), int(d["msg_len"][i])
+        m = d["msg"][o:o + ln].tobytes()
+        assert host.svh_verify_sig(d["pk"][i].tobytes(), d["sig"][i].tobytes(), 64, m, ln) == d["verdict"][i]
+
+
+@pytest.mark.gpu
+def test_gpu_txset_prefetch_matches_replay(host, sv, oracle):
+    if sv.device_count() < 1:
+        pytest.skip("no GPU")
+    host.svh_set_test_verifier(None)
+    host.svh_cache_clear()
+    sign = _oracle_sign_fn(oracle)
+    txs = tg.generate(120, sign, seed=5)
+    tg.add_payload_signatures(txs, sign)
+
+    def verify(pk, sig, msg):
+        return oracle.oracle_ed25519_verify(sig, msg, len(msg), pk) == 0
+
+    want_ok, want_used = tg.replay(txs, verify)
+    ok1, used1, pairs = _check(host, txs, 1)
+    assert (ok1 == want_ok).all() and (used1 == want_used).all()
+    host.svh_cache_clear()
+    ok0, used0, _ = _check(host, txs, 0)
+    assert (ok0 == want_ok).all() and (used0 == want_used).all()
