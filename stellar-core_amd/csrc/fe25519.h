@@ -105,6 +105,27 @@ SV_HD void fe_carry_wide(fe& out, uint64_t h[10]) {
   SV_UNROLL for (int i = 0; i < 10; ++i) out.v[i] = (uint32_t)h[i];
 }
 
+// One 32x32->64 multiply-accumulate = one v_mad_u64_u32.  Written as inline
+// asm so the multiplicands are guaranteed 32-bit VGPRs: with plain C, LLVM
+// promotes limbs merged across branches to i64 and the backend then emits
+// 64x32-bit products (2 v_mad_u64_u32 + 2 v_mov each).  The carry-out SGPR
+// pair is architecturally required on gfx950 (no `null` sdst); vcc is used
+// and never read.
+SV_HD void sv_mad_init(uint64_t& acc, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "vcc");
+#else
+  acc = (uint64_t)a * b;
+#endif
+}
+SV_HD void sv_mad(uint64_t& acc, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
+#else
+  acc += (uint64_t)a * b;
+#endif
+}
+
 // Column sums of f*g (DBL: of 2*f*g).  Wrapped columns (i+j >= 10) carry the
 // factor 2^255 = 19 on g; odd*odd products carry an extra 2 (half-bit radix).
 template <bool DBL>
@@ -115,13 +136,13 @@ SV_HD void fe_mul_cols(uint64_t h[10], const fe& f, const fe& g) {
     fa[i] = DBL ? (f.v[i] << 1) : f.v[i];       // multiplier when not odd*odd
     fb[i] = DBL ? (f.v[i] << 2) : (f.v[i] << 1);  // multiplier for odd*odd
   }
-  SV_UNROLL for (int k = 0; k < 10; ++k) h[k] = 0;
   SV_UNROLL for (int i = 0; i < 10; ++i) {
     SV_UNROLL for (int j = 0; j < 10; ++j) {
       const int k = i + j;
       const uint32_t a = ((i & 1) && (j & 1)) ? fb[i] : fa[i];
       const uint32_t b = (k >= 10) ? g19[j] : g.v[j];
-      h[k >= 10 ? k - 10 : k] += (uint64_t)a * b;
+      if (i == 0) sv_mad_init(h[k], a, b);  // i == 0 opens every column
+      else sv_mad(h[k >= 10 ? k - 10 : k], a, b);
     }
   }
 }
@@ -129,14 +150,14 @@ SV_HD void fe_mul_cols(uint64_t h[10], const fe& f, const fe& g) {
 // Column sums of f^2 (DBL: 2 f^2), using the symmetry f_i f_j = f_j f_i.
 template <bool DBL>
 SV_HD void fe_sq_cols(uint64_t h[10], const fe& f) {
-  SV_UNROLL for (int k = 0; k < 10; ++k) h[k] = 0;
   SV_UNROLL for (int i = 0; i < 10; ++i) {
     SV_UNROLL for (int j = i; j < 10; ++j) {
       const int k = i + j;
       const int sh = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + (DBL ? 1 : 0);
       const uint32_t a = f.v[i] << sh;
       const uint32_t b = (k >= 10) ? 19u * f.v[j] : f.v[j];
-      h[k >= 10 ? k - 10 : k] += (uint64_t)a * b;
+      if (i == 0) sv_mad_init(h[k], a, b);  // i == 0 opens every column
+      else sv_mad(h[k >= 10 ? k - 10 : k], a, b);
     }
   }
 }
