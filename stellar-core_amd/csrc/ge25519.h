@@ -17,7 +17,8 @@
 // ge25519_double_scalarmult_vartime (reference call site:
 // stellar-core src/crypto/SecretKey.cpp:461-463).
 //
-// Limb-bound bookkeeping (see fe25519.h): every fe_mul/fe_sq input is <= M3.
+// Limb-bound bookkeeping (see fe25519.h): every fe_mul/fe_sq input is <= M3,
+// except the f operand of the p1p1 conversions after a doubling (<= M5).
 #pragma once
 
 #include "fe25519.h"
@@ -34,8 +35,11 @@ SV_HD void ge_p2_identity(ge_p2& p) {
   fe_1(p.Z);
 }
 
-// r = 2p.  Inputs R.  Outputs: X R+, Y M2, Z M3, T R+.
-// Operation order frees each input as early as possible (register pressure).
+// r = 2p.  Inputs R.  Outputs: X M5, Y M2, Z M3, T R+.
+// X is left at M5 (one carry pass saved per doubling): the conversions only
+// ever use p1p1 X as the f operand of fe_mul, which tolerates M5 (fe25519.h
+// header; fuzzed at the bound in tests/test_host_arith.py), never as the
+// 19-premultiplied g operand, which needs <= M3.
 SV_HD void ge_dbl(ge_p1p1& r, const fe& X, const fe& Y, const fe& Z) {
   fe XX, YY, ZZ2, A, AA;
   fe_add(A, X, Y);
@@ -45,8 +49,7 @@ SV_HD void ge_dbl(ge_p1p1& r, const fe& X, const fe& Y, const fe& Z) {
   fe_sq2(ZZ2, Z);
   fe_add(r.Y, YY, XX);    // y^2 + x^2            M2
   fe_sub(r.Z, YY, XX);    // y^2 - x^2            M3
-  fe_sub4(r.X, AA, r.Y);  // 2xy = (x+y)^2 - ..  M5 -> R+
-  fe_weak(r.X);
+  fe_sub4(r.X, AA, r.Y);  // 2xy = (x+y)^2 - ..  M5
   fe_sub4(r.T, ZZ2, r.Z); // 2z^2 - (y^2 - x^2)  M5 -> R+
   fe_weak(r.T);
 }
@@ -65,7 +68,8 @@ SV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
 }
 
 // p1p1 -> p3 when the next step is an addition (wantT), else -> p2 (T left
-// stale).  wantT is wave-uniform, so this is a scalar branch.
+// stale).  wantT is wave-uniform, so this is a scalar branch.  Operand order
+// matters: p.X (up to M5 after a doubling) is always the f operand.
 SV_HD void ge_p1p1_to_p3_opt(ge_p3& r, const ge_p1p1& p, bool wantT) {
   if (wantT) fe_mul(r.T, p.X, p.Y);
   fe_mul(r.X, p.X, p.T);
@@ -75,12 +79,19 @@ SV_HD void ge_p1p1_to_p3_opt(ge_p3& r, const ge_p1p1& p, bool wantT) {
 
 // r = p + q where the caller has already swapped q's (Y+X, Y-X) pair for a
 // negative digit (by choosing load addresses); neg then only swaps the final
-// Z/T pair, i.e. negates 2dT.  Same bounds as ge_add_any<false>.
+// Z/T pair, i.e. negates 2dT.  zone: q is affine (Z = 1, base-point table), so
+// 2 Z1 Z2 = 2 Z1 is an add + carry pass instead of a multiply (wave-uniform).
+// Inputs: p R; qa, qb <= M3; qZ, qT2d <= R.  Outputs: X M3, Y M2, Z/T M2 or M3.
 SV_HD void ge_add_preswapped(ge_p1p1& r, const ge_p3& p, const fe& qa, const fe& qb, const fe& qZ,
-                             const fe& qT2d, bool neg) {
+                             const fe& qT2d, bool neg, bool zone) {
   fe t0, t1, PP, MM, TT, ZZ2, zp, zm;
   fe_mul(TT, p.T, qT2d);
-  fe_mul2(ZZ2, p.Z, qZ);  // 2 Z1 Z2, R
+  if (zone) {
+    fe_add(ZZ2, p.Z, p.Z);
+    fe_weak(ZZ2);           // R+
+  } else {
+    fe_mul2(ZZ2, p.Z, qZ);  // 2 Z1 Z2, R
+  }
   fe_add(t0, p.Y, p.X);   // M2
   fe_sub(t1, p.Y, p.X);   // M3
   fe_mul(PP, t0, qa);
@@ -89,39 +100,6 @@ SV_HD void ge_add_preswapped(ge_p1p1& r, const ge_p3& p, const fe& qa, const fe&
   fe_add(r.Y, PP, MM);    // M2
   fe_add(zp, ZZ2, TT);    // M2
   fe_sub(zm, ZZ2, TT);    // M3
-  SV_UNROLL for (int i = 0; i < 10; ++i) {
-    r.Z.v[i] = neg ? zm.v[i] : zp.v[i];
-    r.T.v[i] = neg ? zp.v[i] : zm.v[i];
-  }
-}
-
-// r = p + (neg ? -q : q), q given as (YpX, YmX, T2d) plus either its Z
-// (ZONE = false, cached form) or Z = 1 (ZONE = true, affine precomp form).
-// p inputs R.  q: YpX <= M3, YmX <= M3, Z and T2d <= R.
-// Outputs: X M3, Y M2, Z/T M2 or M3.
-template <bool ZONE>
-SV_HD void ge_add_any(ge_p1p1& r, const ge_p3& p, const fe& qYpX, const fe& qYmX, const fe& qZ,
-                      const fe& qT2d, bool neg) {
-  fe t0, t1, a, b, PP, MM, TT, ZZ2, zp, zm;
-  fe_add(t0, p.Y, p.X);  // M2
-  fe_sub(t1, p.Y, p.X);  // M3
-  SV_UNROLL for (int i = 0; i < 10; ++i) {
-    a.v[i] = neg ? qYmX.v[i] : qYpX.v[i];
-    b.v[i] = neg ? qYpX.v[i] : qYmX.v[i];
-  }
-  fe_mul(PP, t0, a);
-  fe_mul(MM, t1, b);
-  fe_mul(TT, p.T, qT2d);
-  if (ZONE) {
-    fe_add(ZZ2, p.Z, p.Z);
-    fe_weak(ZZ2);  // R+
-  } else {
-    fe_mul2(ZZ2, p.Z, qZ);  // 2 Z1 Z2, R
-  }
-  fe_sub(r.X, PP, MM);  // M3
-  fe_add(r.Y, PP, MM);  // M2
-  fe_add(zp, ZZ2, TT);  // M2
-  fe_sub(zm, ZZ2, TT);  // M3
   SV_UNROLL for (int i = 0; i < 10; ++i) {
     r.Z.v[i] = neg ? zm.v[i] : zp.v[i];
     r.T.v[i] = neg ? zp.v[i] : zm.v[i];
@@ -192,12 +170,18 @@ SV_COLD bool ge_frombytes(ge_p3& h, const uint32_t w[8], bool negate) {
   return m_ok || p_ok;
 }
 
-// canonical encoding of a projective point (8 little-endian words)
-SV_COLD void ge_p2_tobytes(uint32_t out[8], const fe& X, const fe& Y, const fe& Z) {
-  fe zi, x, y;
-  fe_invert(zi, Z);
+// canonical encoding of a projective point given 1/Z (8 little-endian words)
+SV_COLD void ge_p2_tobytes_zinv(uint32_t out[8], const fe& X, const fe& Y, const fe& zi) {
+  fe x, y;
   fe_mul(x, X, zi);
   fe_mul(y, Y, zi);
   fe_tobytes(out, y);
   out[7] ^= fe_isnegative(x) << 31;
+}
+
+// canonical encoding of a projective point (8 little-endian words)
+SV_COLD void ge_p2_tobytes(uint32_t out[8], const fe& X, const fe& Y, const fe& Z) {
+  fe zi;
+  fe_invert(zi, Z);
+  ge_p2_tobytes_zinv(out, X, Y, zi);
 }

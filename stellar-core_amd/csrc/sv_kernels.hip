@@ -7,11 +7,11 @@
 // ballot word of the verdict bitmap per wave iteration).
 //
 // Memory per workgroup: the 129-entry base-point table (18.6 KiB) in LDS.
-// Memory per lane: a 1728 B slot of the HBM workspace for the signature's
-// 9-entry table of multiples of -A, lane-major: lanes gather different
-// entries (per-lane digits), so keeping each lane's entry contiguous (192 B)
-// is what bounds the line traffic (a wave-interleaved layout measured ~8x
-// line amplification, profiles/r01_*).
+// Memory per lane: a 2304 B slot of the HBM workspace: the signature's 9-entry
+// table of multiples of -A (1728 B) + SV_BATCH_K parked projective points.
+// Lane-major: lanes gather different entries (per-lane digits), so keeping
+// each lane's entry contiguous (192 B) is what bounds the line traffic (a
+// wave-interleaved layout measured ~4x more L2-miss traffic, profiles/r01/).
 #include <hip/hip_runtime.h>
 
 #include "verify_core.h"
@@ -29,7 +29,7 @@ struct sv_kparams {
   uint32_t fixed_len;     // 0 = variable-length
   uint8_t* verdict;       // n bytes
   uint64_t* bitmap;       // optional, ceil(n/64) words
-  sv_u4* ws;              // workspace: grid threads x 9 entries x 12 quads (lane-major)
+  sv_u4* ws;              // workspace: grid threads x SV_SLOT_QUADS (lane-major)
   const sv_u4* btab;      // SV_BTAB_ENTRIES x 9 quads (global copy)
 };
 
@@ -44,6 +44,31 @@ __device__ __forceinline__ void sv_unpack2(uint32_t w[8], const sv_u4* p) {
   w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
 }
 
+// Loads one signature's inputs and hashes R || A || M (step (6)).
+template <int MODE>
+__device__ __forceinline__ void sv_load_and_hash(const sv_kparams& p, uint64_t ii, uint32_t A[8], uint32_t S[8],
+                                                 uint32_t hram[16]) {
+  uint32_t R[8];
+  sv_unpack2(A, p.pk + 2 * ii);
+  sv_unpack2(R, p.sig + 4 * ii);
+  sv_unpack2(S, p.sig + 4 * ii + 2);
+  if (MODE == 0) {
+    uint32_t M[8];
+    sv_unpack2(M, (const sv_u4*)(p.msg) + 2 * ii);
+    sha512_ram32(hram, R, A, M);
+  } else if (MODE == 1) {
+    sha512_ram_var(hram, R, A, p.msg + p.msg_off[ii], p.msg_len[ii]);
+  } else {
+    sha512_ram_var(hram, R, A, p.msg + ii * (uint64_t)p.fixed_len, p.fixed_len);
+  }
+}
+
+// Each wave iteration handles SV_BATCH_K groups of 64 consecutive signatures
+// (group k at base + k*stride); each lane runs steps (1)-(7) for its K
+// signatures, parks the projective results in its workspace slot, then
+// inverts all K Z coordinates with ONE exponentiation (Montgomery's trick)
+// and finishes step (8).  Groups entirely past n are skipped (wave-uniform)
+// and enter the batch inversion as Z = 1.
 template <int MODE>  // 0: fixed 32-byte messages, 1: variable length, 2: fixed other length
 __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_kernel(sv_kparams p) {
   __shared__ sv_u4 s_btab[SV_BTAB_ENTRIES * (SV_BTAB_STRIDE / 4)];
@@ -51,31 +76,52 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_kernel(
 
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // lane-major workspace slot: this lane's 9 table entries, 1728 contiguous bytes
-  sv_u4* slot = p.ws + gtid * (SV_ATAB_ENTRIES * SV_ATAB_QUADS);
+  // lane-major workspace slot: table_A (1728 B) + K pending points
+  sv_u4* slot = p.ws + gtid * SV_SLOT_QUADS;
+  sv_u4* pend = slot + SV_ATAB_ENTRIES * SV_ATAB_QUADS;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
 
-  for (uint64_t base = gtid - lane; base < p.n; base += stride) {
-    const uint64_t i = base + lane;
-    const bool active = i < p.n;
-    const uint64_t ii = active ? i : p.n - 1;  // idle tail lanes redo the last item
-    uint32_t A[8], R[8], S[8], hram[16];
-    sv_unpack2(A, p.pk + 2 * ii);
-    sv_unpack2(R, p.sig + 4 * ii);
-    sv_unpack2(S, p.sig + 4 * ii + 2);
-    if (MODE == 0) {
-      uint32_t M[8];
-      sv_unpack2(M, (const sv_u4*)(p.msg) + 2 * ii);
-      sha512_ram32(hram, R, A, M);
-    } else if (MODE == 1) {
-      sha512_ram_var(hram, R, A, p.msg + p.msg_off[ii], p.msg_len[ii]);
-    } else {
-      sha512_ram_var(hram, R, A, p.msg + ii * (uint64_t)p.fixed_len, p.fixed_len);
+  for (uint64_t base = gtid - lane; base < p.n; base += SV_BATCH_K * stride) {
+    uint32_t okmask = 0;
+    int ngroups = 0;
+    SV_NOUNROLL for (int k = 0; k < SV_BATCH_K; ++k) {
+      const uint64_t gbase = base + (uint64_t)k * stride;
+      if (gbase >= p.n) break;  // wave-uniform
+      ngroups = k + 1;
+      const uint64_t i = gbase + lane;
+      const uint64_t ii = i < p.n ? i : p.n - 1;  // idle tail lanes redo the last item
+      uint32_t A[8], S[8], hram[16];
+      sv_load_and_hash<MODE>(p, ii, A, S, hram);
+      ge_p3 P;
+      const bool ok = sv_verify_pre(P, A, p.sig + 4 * ii, S, hram, slot, 1, s_btab);
+      okmask |= (ok ? 1u : 0u) << k;
+      sv_store_fe3(pend + k * SV_PEND_QUADS, 1, P.X);
+      sv_store_fe3(pend + k * SV_PEND_QUADS + 3, 1, P.Y);
+      sv_store_fe3(pend + k * SV_PEND_QUADS + 6, 1, P.Z);
     }
-    const bool ok = sv_verify_core(A, p.sig + 4 * ii, S, hram, slot, 1, s_btab) && active;
-    if (active) p.verdict[i] = ok ? 1 : 0;
-    const uint64_t mask = __ballot(ok);
-    if (p.bitmap != nullptr && lane == 0) p.bitmap[base >> 6] = mask;
+    {
+      fe z[SV_BATCH_K], zi[SV_BATCH_K];
+      SV_UNROLL for (int k = 0; k < SV_BATCH_K; ++k) {
+        if (k < ngroups) sv_load_fe3(z[k], pend + k * SV_PEND_QUADS + 6, 1);
+        else fe_1(z[k]);
+      }
+      fe_batch_invert<SV_BATCH_K>(zi, z);
+      SV_UNROLL for (int k = 0; k < SV_BATCH_K; ++k) sv_store_fe3(pend + k * SV_PEND_QUADS + 6, 1, zi[k]);
+    }
+    SV_NOUNROLL for (int k = 0; k < ngroups; ++k) {
+      const uint64_t gbase = base + (uint64_t)k * stride;
+      const uint64_t i = gbase + lane;
+      const bool active = i < p.n;
+      const uint64_t ii = active ? i : p.n - 1;
+      fe X, Y, zi;
+      sv_load_fe3(X, pend + k * SV_PEND_QUADS, 1);
+      sv_load_fe3(Y, pend + k * SV_PEND_QUADS + 3, 1);
+      sv_load_fe3(zi, pend + k * SV_PEND_QUADS + 6, 1);
+      const bool ok = ((okmask >> k) & 1u) && sv_encode_matches(X, Y, zi, p.sig + 4 * ii) && active;
+      if (active) p.verdict[i] = ok ? 1 : 0;
+      const uint64_t mask = __ballot(ok);
+      if (p.bitmap != nullptr && lane == 0) p.bitmap[gbase >> 6] = mask;
+    }
   }
 }
 
@@ -99,7 +145,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_sign_kernel(sv
   sv_load_btab_lds(s_btab, p.btab);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  sv_u4* slot = p.ws + gtid * (SV_ATAB_ENTRIES * SV_ATAB_QUADS);
+  sv_u4* slot = p.ws + gtid * SV_SLOT_QUADS;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = gtid - lane; base < p.n; base += stride) {
     const uint64_t i = base + lane;
@@ -121,9 +167,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_sign_kernel(sv
 // ------------------------------------------------------------ launchers
 extern "C" {
 
-size_t sv_ws_bytes_per_block(void) {
-  return (size_t)(SV_BLOCK / 64) * SV_ATAB_ENTRIES * SV_ATAB_QUADS * 64 * sizeof(sv_u4);
-}
+size_t sv_ws_bytes_per_block(void) { return (size_t)SV_BLOCK * SV_SLOT_QUADS * sizeof(sv_u4); }
 size_t sv_btab_bytes(void) { return (size_t)SV_BTAB_DWORDS * 4; }
 int sv_block_threads(void) { return SV_BLOCK; }
 

@@ -40,6 +40,11 @@ struct __attribute__((aligned(16))) sv_u4 {
 // A-table (HBM workspace): 9 entries x 12 quads: YpX YmX Z T2d (3 quads each)
 #define SV_ATAB_ENTRIES 9
 #define SV_ATAB_QUADS 12
+// Signatures per lane whose final inversions are batched (Montgomery trick),
+// and the per-lane workspace slot: table_A + K pending points (X, Y, Z).
+#define SV_BATCH_K 4
+#define SV_PEND_QUADS 9
+#define SV_SLOT_QUADS (SV_ATAB_ENTRIES * SV_ATAB_QUADS + SV_BATCH_K * SV_PEND_QUADS)
 
 SV_HD bool sv_small_order(const uint32_t s[8]) {
   const uint32_t bl[7][8] = {
@@ -96,29 +101,27 @@ SV_COLD void sv_build_atab(sv_u4* slot, int qstride, const ge_p3& negA) {
   ge_p3 P3 = negA;
   ge_p1p1 Q;
   SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
-    ge_add_any<false>(Q, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false);
+    ge_add_preswapped(Q, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, false);
     ge_p1p1_to_p3(P3, Q);
     ge_p3_to_cached(ce, P3);
     sv_store_cached(slot, qstride, e, ce);
   }
 }
 
-// Builds table_A for -A in the lane's workspace slot and computes
-// enc = encode([h](-A) + [S]B)  (step (7) and the encoding half of (8)).
+// Builds table_A for -A in the lane's workspace slot and computes the
+// projective point Rp = [h](-A) + [S]B  (step (7)).
 //
 // Step machine: per window w (64 of them, MSB first) run steps
 //   s = 0..3  doubling, s = 4  add table_A[d_A], s = 5 (even w) add table_B[d_B]
 // with one code instance of each step kind; every branch is wave-uniform.
-SV_HD void sv_double_scalarmult_encode(uint32_t enc[8], const ge_p3& negA, const uint32_t h[8],
-                                       const uint32_t S[8], sv_u4* slot, int qstride,
-                                       const sv_u4* btab) {
+SV_HD void sv_double_scalarmult(ge_p3& P, const ge_p3& negA, const uint32_t h[8], const uint32_t S[8],
+                                sv_u4* slot, int qstride, const sv_u4* btab) {
   sv_build_atab(slot, qstride, negA);
 
   uint32_t da[8], db[8];
   sc_digits_r16(da, h);
   sc_digits_r256(db, S);
 
-  ge_p3 P;
   fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
   ge_p1p1 Q;
   SV_NOUNROLL for (int w = 63; w >= 0; --w) {
@@ -131,7 +134,8 @@ SV_HD void sv_double_scalarmult_encode(uint32_t enc[8], const ge_p3& negA, const
         // a doubling leaves no room for 40 more live VGPRs at 2 waves/SIMD)
         fe qa, qb, qz, qt;
         bool neg;
-        if (s == 4) {
+        const bool zone = s == 5;
+        if (!zone) {
           const int32_t d = sc_pop_top(da, 4);
           neg = d < 0;
           const sv_u4* e = slot + (neg ? -d : d) * SV_ATAB_QUADS * qstride;
@@ -148,19 +152,28 @@ SV_HD void sv_double_scalarmult_encode(uint32_t enc[8], const ge_p3& negA, const
           fe_1(qz);
           sv_load_fe3(qt, e + 6, 1);
         }
-        ge_add_preswapped(Q, P, qa, qb, qz, qt, neg);
+        ge_add_preswapped(Q, P, qa, qb, qz, qt, neg, zone);
       }
       ge_p1p1_to_p3_opt(P, Q, s + 1 >= 4 && s + 1 < nsteps);
     }
   }
+}
+
+SV_HD void sv_double_scalarmult_encode(uint32_t enc[8], const ge_p3& negA, const uint32_t h[8],
+                                       const uint32_t S[8], sv_u4* slot, int qstride,
+                                       const sv_u4* btab) {
+  ge_p3 P;
+  sv_double_scalarmult(P, negA, h, S, slot, qstride, btab);
   ge_p2_tobytes(enc, P.X, P.Y, P.Z);
 }
 
-// Steps (1)-(8) given the SHA-512(R||A||M) digest as a 512-bit LE integer.
-// R is read twice from memory (Rp: its 2 quads) rather than kept live in
-// VGPRs across the scalar multiplication.
-SV_HD bool sv_verify_core(const uint32_t A[8], const sv_u4* Rp, const uint32_t S[8],
-                          const uint32_t hram[16], sv_u4* slot, int qstride, const sv_u4* btab) {
+// Steps (1)-(7) given the SHA-512(R||A||M) digest as a 512-bit LE integer:
+// returns the verdict of checks (1)-(5) and the projective R' in P.  For a
+// lane rejected by (1)-(5), P.Z is set to 1 so that a batch inversion over
+// several signatures (sv_finalize_batch) can never be poisoned by a garbage
+// point; its encoding is irrelevant to its (already false) verdict.
+SV_HD bool sv_verify_pre(ge_p3& P, const uint32_t A[8], const sv_u4* Rp, const uint32_t S[8],
+                         const uint32_t hram[16], sv_u4* slot, int qstride, const sv_u4* btab) {
   bool ok;
   {
     uint32_t R[8];
@@ -179,12 +192,46 @@ SV_HD bool sv_verify_core(const uint32_t A[8], const sv_u4* Rp, const uint32_t S
   uint32_t Sc[8];
   SV_UNROLL for (int i = 0; i < 8; ++i) Sc[i] = S[i];
   Sc[7] &= 0x0fffffffu;
+  sv_double_scalarmult(P, negA, h, Sc, slot, qstride, btab);
+  if (!ok) fe_1(P.Z);
+  return ok;
+}
+
+// Step (8): encode(X/Z, Y/Z) == R, given zi = 1/Z.
+SV_HD bool sv_encode_matches(const fe& X, const fe& Y, const fe& zi, const sv_u4* Rp) {
   uint32_t enc[8];
-  sv_double_scalarmult_encode(enc, negA, h, Sc, slot, qstride, btab);
+  ge_p2_tobytes_zinv(enc, X, Y, zi);
   const sv_u4 r0 = Rp[0], r1 = Rp[1];
   const uint32_t diff = (enc[0] ^ r0.x) | (enc[1] ^ r0.y) | (enc[2] ^ r0.z) | (enc[3] ^ r0.w) |
                         (enc[4] ^ r1.x) | (enc[5] ^ r1.y) | (enc[6] ^ r1.z) | (enc[7] ^ r1.w);
-  return ok && diff == 0;
+  return diff == 0;
+}
+
+// Steps (1)-(8) for one signature (single inversion).  R is read from memory
+// (Rp: its 2 quads) rather than kept live across the scalar multiplication.
+SV_HD bool sv_verify_core(const uint32_t A[8], const sv_u4* Rp, const uint32_t S[8],
+                          const uint32_t hram[16], sv_u4* slot, int qstride, const sv_u4* btab) {
+  ge_p3 P;
+  const bool ok = sv_verify_pre(P, A, Rp, S, hram, slot, qstride, btab);
+  fe zi;
+  fe_invert(zi, P.Z);
+  return sv_encode_matches(P.X, P.Y, zi, Rp) && ok;
+}
+
+// Montgomery's simultaneous inversion: zi[k] = 1/z[k] for K field elements
+// with one exponentiation and 3(K-1) multiplications (every z[k] != 0).
+template <int K>
+SV_HD void fe_batch_invert(fe zi[K], const fe z[K]) {
+  fe c[K];
+  c[0] = z[0];
+  SV_UNROLL for (int k = 1; k < K; ++k) fe_mul(c[k], c[k - 1], z[k]);
+  fe inv;
+  fe_invert(inv, c[K - 1]);
+  SV_UNROLL for (int k = K - 1; k > 0; --k) {
+    fe_mul(zi[k], inv, c[k - 1]);
+    fe_mul(inv, inv, z[k]);
+  }
+  zi[0] = inv;
 }
 
 // Base-point table entry e = e·B in affine precomp form (used at init).
@@ -200,7 +247,7 @@ SV_HD void sv_btab_entry(uint32_t out[SV_BTAB_STRIDE], int e) {
   fe_0(acc.X); fe_1(acc.Y); fe_1(acc.Z); fe_0(acc.T);
   ge_p1p1 Q;
   for (int i = 0; i < e; ++i) {
-    ge_add_any<false>(Q, acc, bc.YpX, bc.YmX, bc.Z, bc.T2d, false);
+    ge_add_preswapped(Q, acc, bc.YpX, bc.YmX, bc.Z, bc.T2d, false, false);
     ge_p1p1_to_p3(acc, Q);
   }
   fe zi, x, y, xy, d2, ypx, ymx, xy2d;

@@ -93,6 +93,41 @@ void hc_btab(uint32_t* out) {
   memcpy(out, g_btab.data(), SV_BTAB_DWORDS * 4);
 }
 
+// Same grouping as sv_verify_kernel: K = SV_BATCH_K signatures share one
+// inversion (fe_batch_invert); rejected rows park Z = 1 (sv_verify_pre).
+void hc_verify_batch_grouped(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                             const uint32_t* len, size_t n, uint8_t* verdict) {
+  std::call_once(g_once, init_btab);
+  std::vector<sv_u4> slot(SV_SLOT_QUADS);
+  for (size_t base = 0; base < n; base += SV_BATCH_K) {
+    ge_p3 P[SV_BATCH_K];
+    bool ok[SV_BATCH_K];
+    fe z[SV_BATCH_K], zi[SV_BATCH_K];
+    for (int k = 0; k < SV_BATCH_K; ++k) {
+      const size_t i = base + k;
+      if (i >= n) {
+        fe_1(z[k]);
+        ok[k] = false;
+        continue;
+      }
+      uint32_t A[8], S[8], hram[16];
+      alignas(16) uint32_t R[8];
+      load_words(A, pk + 32 * i);
+      load_words(R, sig + 64 * i);
+      load_words(S, sig + 64 * i + 32);
+      sha512_ram_var(hram, R, A, msg + off[i], len[i]);
+      ok[k] = sv_verify_pre(P[k], A, (const sv_u4*)R, S, hram, slot.data(), 1, (const sv_u4*)g_btab.data());
+      z[k] = P[k].Z;
+    }
+    fe_batch_invert<SV_BATCH_K>(zi, z);
+    for (int k = 0; k < SV_BATCH_K && base + k < n; ++k) {
+      alignas(16) uint32_t R[8];
+      load_words(R, sig + 64 * (base + k));
+      verdict[base + k] = (ok[k] && sv_encode_matches(P[k].X, P[k].Y, zi[k], (const sv_u4*)R)) ? 1 : 0;
+    }
+  }
+}
+
 void hc_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
                      const uint32_t* len, size_t n, uint8_t* verdict) {
   std::call_once(g_once, init_btab);

@@ -67,6 +67,22 @@ def test_fe_limb_bounds_worst_case(hostcore):
         assert _words(o) == _val(big) % P
 
 
+def test_fe_mul_m5_f_operand(hostcore):
+    """ge_dbl leaves r.X at M5 (= AA + 4p - (YY+XX)); it is only ever the f
+    operand of fe_mul (g, the operand pre-multiplied by 19, stays <= M3)."""
+    rnd = random.Random(7)
+    o = (ctypes.c_uint32 * 8)()
+    for trial in range(400):
+        if trial < 10:
+            lf = [5 * (1 << w) - 1 for w in W]
+            lg = [3 * (1 << w) - 1 for w in W]
+        else:
+            lf = [rnd.randrange(5 * (1 << w)) for w in W]
+            lg = [rnd.randrange(3 * (1 << w)) for w in W]
+        hostcore.hc_fe_mul_limbs(o, (ctypes.c_uint32 * 10)(*lf), (ctypes.c_uint32 * 10)(*lg), 0)
+        assert _words(o) == _val(lf) * _val(lg) % P
+
+
 def test_fe_tobytes_edge_values(hostcore):
     o = (ctypes.c_uint32 * 8)()
     for v in [0, 1, P - 1, P, P + 1, P + 18, 2**255 - 1, 2 * P - 1]:
@@ -132,6 +148,26 @@ def _host_verify(hostcore, d, rows):
                              ctypes.c_void_p(ln.ctypes.data), ctypes.c_size_t(len(rows)),
                              ctypes.c_void_p(out.ctypes.data))
     return out
+
+
+def test_grouped_batch_inversion_matches_golden(hostcore, golden):
+    """The kernel's K-signature batch inversion (with rejected rows parked at
+    Z = 1) must give the same verdicts: adversarial rows interleave accepts and
+    rejects inside every group."""
+    for name in ("adversarial", "intree"):
+        d = golden[name]
+        rows = np.arange(len(d["verdict"]))[::4] if name == "adversarial" else np.arange(len(d["verdict"]))
+        pk = np.ascontiguousarray(d["pk"][rows])
+        sig = np.ascontiguousarray(d["sig"][rows])
+        off = np.ascontiguousarray(d["msg_off"][rows])
+        ln = np.ascontiguousarray(d["msg_len"][rows])
+        msg = np.ascontiguousarray(d["msg"])
+        out = np.zeros(len(rows), np.uint8)
+        hostcore.hc_verify_batch_grouped(ctypes.c_void_p(pk.ctypes.data), ctypes.c_void_p(sig.ctypes.data),
+                                         ctypes.c_void_p(msg.ctypes.data), ctypes.c_void_p(off.ctypes.data),
+                                         ctypes.c_void_p(ln.ctypes.data), ctypes.c_size_t(len(rows)),
+                                         ctypes.c_void_p(out.ctypes.data))
+        assert np.array_equal(out, d["verdict"][rows]), name
 
 
 def test_lane_verifier_matches_golden(hostcore, golden):
