@@ -171,6 +171,10 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
     sv = importlib.import_module("stellar-core_amd")
+    # one process per GPU: rank -> device LOCAL_RANK.  SV_BENCH_SHARE_GPUS=1
+    # (rehearsal only) maps ranks onto the visible devices modulo their count.
+    if os.environ.get("SV_BENCH_SHARE_GPUS") == "1":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -236,11 +240,16 @@ def main():
     bitmap_ok = bool((d_bitmap[:full] == -1).all().item())
     verdicts_ok = verdict_count == n and bitmap_ok
 
+    global_digest = None
     if world > 1:
         t = torch.tensor([elapsed, 0.0 if verdicts_ok else 1.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, bad = float(t[0]), float(t[1])
         verdicts_ok = bad == 0.0
+        # host gather of every rank's verdict slice (outside the timed region)
+        sh = importlib.import_module("stellar-core_amd.sharding")
+        full = sh.gather_verdicts(d_verdict.cpu().numpy(), n * world, world, rank)
+        global_digest = sh.verdict_digest(full)
     total = n * world * args.steps
     value = total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
@@ -284,6 +293,7 @@ def main():
             },
             "verdicts_ok": verdicts_ok,
             "dataset_digest_ok": digest_ok,
+            "gathered_verdict_digest": global_digest,
             "kernel": {"ms_per_launch": kernel_ms, "launches": k_launches, "verifies_per_s": kernel_rate},
             "roofline": {
                 "bound": "valu-int",

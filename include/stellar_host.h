@@ -15,6 +15,10 @@
  *                              (/root/reference/src/transactions/SignatureChecker.cpp:30-158),
  *                              optionally after one GPU batch pre-pass over the
  *                              whole set
+ *   svh_mb_run              == VerifyMicroBatcher driven by `producers` threads: the
+ *                              SCP/overlay pre-verify (/root/reference/src/overlay/
+ *                              Peer.cpp:963-970) turned into size/deadline-flushed
+ *                              GPU batches
  */
 #ifndef STELLAR_HOST_H
 #define STELLAR_HOST_H
@@ -71,6 +75,16 @@ void svh_engine_counts(uint64_t* signatures, uint64_t* batches);
 void svh_set_test_verifier(svh_batch_verify_fn fn);
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs);
+
+typedef struct svh_mb_stats {
+  uint64_t items, batches, flushed_by_size, flushed_by_deadline, max_batch;
+  double lat_p50_us, lat_p99_us; /* submit -> verdict ready */
+} svh_mb_stats;
+/* Feed n signatures through a VerifyMicroBatcher from `producers` threads
+ * (item i from thread i % producers, optional sleep between submissions). */
+int svh_mb_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+               const uint32_t* msg_len, size_t n, int producers, uint32_t max_batch, uint32_t max_delay_us,
+               uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats);
 
 #ifdef __cplusplus
 }

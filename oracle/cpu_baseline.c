@@ -67,3 +67,53 @@ double cpubase_run(const char* sodium_path, const uint8_t* pk, const uint8_t* si
   clock_gettime(CLOCK_MONOTONIC, &t1);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* libsodium-backed batch verifier with the svh_batch_verify_fn signature
+ * (include/stellar_host.h), so the C++ SignatureChecker mirror can be timed
+ * on the reference's own CPU path (one libsodium call per signature, on
+ * `g_threads` threads).  Set up with cpubase_set_sodium(path, threads). */
+static verify_fn g_sodium_fn = 0;
+static int g_threads = 1;
+
+int cpubase_set_sodium(const char* sodium_path, int threads) {
+  void* h = dlopen(sodium_path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) return -1;
+  int (*init)(void) = (int (*)(void))dlsym(h, "sodium_init");
+  g_sodium_fn = (verify_fn)dlsym(h, "crypto_sign_verify_detached");
+  if (!init || !g_sodium_fn || init() < 0) return -2;
+  g_threads = threads < 1 ? 1 : (threads > 256 ? 256 : threads);
+  return 0;
+}
+
+struct vjob {
+  const uint8_t *pk, *sig, *msg;
+  const uint64_t* off;
+  const uint32_t* len;
+  size_t lo, hi;
+  uint8_t* out;
+};
+
+static void* vworker(void* arg) {
+  struct vjob* j = (struct vjob*)arg;
+  for (size_t i = j->lo; i < j->hi; ++i)
+    j->out[i] = g_sodium_fn(j->sig + 64 * i, j->msg + j->off[i], j->len[i], j->pk + 32 * i) == 0;
+  return 0;
+}
+
+int cpubase_sodium_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                         const uint32_t* len, size_t n, uint8_t* verdict) {
+  if (!g_sodium_fn) return -1;
+  int T = g_threads;
+  if ((size_t)T > n) T = n ? (int)n : 1;
+  pthread_t th[256];
+  struct vjob jobs[256];
+  for (int t = 0; t < T; ++t) {
+    jobs[t].pk = pk; jobs[t].sig = sig; jobs[t].msg = msg; jobs[t].off = off; jobs[t].len = len;
+    jobs[t].lo = (size_t)t * n / T;
+    jobs[t].hi = (size_t)(t + 1) * n / T;
+    jobs[t].out = verdict;
+    if (pthread_create(&th[t], 0, vworker, &jobs[t]) != 0) return -3;
+  }
+  for (int t = 0; t < T; ++t) pthread_join(th[t], 0);
+  return 0;
+}

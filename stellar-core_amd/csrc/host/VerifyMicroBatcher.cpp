@@ -1,0 +1,92 @@
+// See VerifyMicroBatcher.h.
+#include "VerifyMicroBatcher.h"
+
+#include <algorithm>
+#include <exception>
+
+namespace stellar {
+
+VerifyMicroBatcher::VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay)
+    : mMaxBatch(std::max<size_t>(1, maxBatch)), mMaxDelay(maxDelay), mWorker([this] { run(); }) {}
+
+VerifyMicroBatcher::~VerifyMicroBatcher() {
+  {
+    std::lock_guard<std::mutex> g(mMu);
+    mStop = true;
+  }
+  mCv.notify_all();
+  mWorker.join();
+}
+
+std::future<bool> VerifyMicroBatcher::submit(PublicKey const& key, Signature const& sig, ByteSlice const& msg) {
+  Item it;
+  it.key = key;
+  it.sig = sig;
+  it.msg.assign(msg.begin(), msg.end());
+  it.t0 = std::chrono::steady_clock::now();
+  std::future<bool> f = it.done.get_future();
+  bool wake;
+  {
+    std::lock_guard<std::mutex> g(mMu);
+    mQueue.push_back(std::move(it));
+    ++mStats.items;
+    wake = mQueue.size() == 1 || mQueue.size() >= mMaxBatch;
+  }
+  if (wake) mCv.notify_one();
+  return f;
+}
+
+VerifyMicroBatcher::Stats VerifyMicroBatcher::stats() const {
+  std::lock_guard<std::mutex> g(mMu);
+  return mStats;
+}
+
+std::vector<double> VerifyMicroBatcher::latencies() const {
+  std::lock_guard<std::mutex> g(mMu);
+  return mLatUs;
+}
+
+void VerifyMicroBatcher::run() {
+  std::unique_lock<std::mutex> lk(mMu);
+  for (;;) {
+    // wait for: stop, a full batch, or the oldest item's deadline
+    while (!mStop && mQueue.empty()) mCv.wait(lk);
+    if (mQueue.empty() && mStop) return;
+    bool bySize = mQueue.size() >= mMaxBatch;
+    if (!bySize && !mStop) {
+      const auto deadline = mQueue.front().t0 + mMaxDelay;
+      mCv.wait_until(lk, deadline, [&] { return mStop || mQueue.size() >= mMaxBatch; });
+      bySize = mQueue.size() >= mMaxBatch;
+    }
+    const size_t take = std::min(mQueue.size(), mMaxBatch);
+    std::vector<Item> batch;
+    batch.reserve(take);
+    for (size_t i = 0; i < take; ++i) {
+      batch.push_back(std::move(mQueue.front()));
+      mQueue.pop_front();
+    }
+    ++mStats.batches;
+    if (bySize) ++mStats.flushedBySize;
+    else ++mStats.flushedByDeadline;
+    mStats.maxBatchSeen = std::max<uint64_t>(mStats.maxBatchSeen, take);
+    lk.unlock();
+    std::vector<PubKeyUtils::VerifyItem> items;
+    items.reserve(take);
+    for (auto& b : batch) items.push_back(PubKeyUtils::VerifyItem{&b.key, &b.sig, ByteSlice(b.msg)});
+    std::vector<double> lat(take);
+    try {
+      std::vector<bool> v = PubKeyUtils::verifySigBatch(items);
+      const auto now = std::chrono::steady_clock::now();
+      for (size_t i = 0; i < take; ++i) {
+        lat[i] = std::chrono::duration<double, std::micro>(now - batch[i].t0).count();
+        batch[i].done.set_value(v[i]);
+      }
+    } catch (...) {
+      for (auto& b : batch) b.done.set_exception(std::current_exception());
+    }
+    lk.lock();
+    mLatUs.insert(mLatUs.end(), lat.begin(), lat.end());
+  }
+}
+
+}  // namespace stellar

@@ -1,0 +1,68 @@
+// Micro-batcher for latency-bound single verifications.
+//
+// Reference pattern it replaces: the overlay thread pre-verifies every
+// SCP_MESSAGE signature one by one and discards the result only to warm the
+// global verify cache (/root/reference/src/overlay/Peer.cpp:963-970); the main
+// thread's HerderImpl::verifyEnvelope (src/herder/HerderImpl.cpp:2414-2432)
+// then hits the cache.  Here producers enqueue (pk, sig, msg) and get a
+// future; one worker thread flushes the queue as ONE PubKeyUtils::verifySigBatch
+// call (which also fills the cache) when it holds maxBatch items or when the
+// oldest item has waited maxDelay -- whichever comes first.
+#pragma once
+
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <future>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "PubKeyUtils.h"
+
+namespace stellar {
+
+class VerifyMicroBatcher {
+ public:
+  VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay);
+  ~VerifyMicroBatcher();  // drains the queue, then stops the worker
+  VerifyMicroBatcher(VerifyMicroBatcher const&) = delete;
+  VerifyMicroBatcher& operator=(VerifyMicroBatcher const&) = delete;
+
+  // Thread-safe.  The future carries the verdict, or VerifyEngineError.
+  std::future<bool> submit(PublicKey const& key, Signature const& sig, ByteSlice const& msg);
+
+  struct Stats {
+    uint64_t items = 0;
+    uint64_t batches = 0;
+    uint64_t flushedBySize = 0;
+    uint64_t flushedByDeadline = 0;
+    uint64_t maxBatchSeen = 0;
+  };
+  Stats stats() const;
+  // submit -> verdict-ready latencies in microseconds (recorded per item)
+  std::vector<double> latencies() const;
+
+ private:
+  struct Item {
+    PublicKey key;
+    Signature sig;
+    std::vector<uint8_t> msg;
+    std::promise<bool> done;
+    std::chrono::steady_clock::time_point t0;
+  };
+  void run();
+
+  const size_t mMaxBatch;
+  const std::chrono::microseconds mMaxDelay;
+  mutable std::mutex mMu;
+  std::condition_variable mCv;
+  std::deque<Item> mQueue;
+  bool mStop = false;
+  Stats mStats;
+  std::vector<double> mLatUs;
+  std::thread mWorker;
+};
+
+}  // namespace stellar

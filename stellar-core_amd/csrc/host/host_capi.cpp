@@ -9,6 +9,12 @@
 #include "../../../include/stellar_host.h"
 #include "PubKeyUtils.h"
 #include "SignatureChecker.h"
+#include "VerifyMicroBatcher.h"
+
+#include <algorithm>
+#include <chrono>
+#include <future>
+#include <thread>
 #include "hashes.h"
 
 using namespace stellar;
@@ -120,6 +126,57 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
       SignatureChecker c(txs[t].protocol, hashes[t], dsigs[t], use_prefetch ? &pre : nullptr);
       ok[t] = c.checkSignature(sgn[t], txs[t].needed_weight) ? 1 : 0;
       all_used[t] = c.checkAllSignaturesUsed() ? 1 : 0;
+    }
+    return SVH_OK;
+  } catch (std::exception const& e) {
+    return guard_exc(e);
+  }
+}
+
+int svh_mb_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+               const uint32_t* msg_len, size_t n, int producers, uint32_t max_batch, uint32_t max_delay_us,
+               uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats) {
+  try {
+    if (producers < 1) producers = 1;
+    std::vector<int> err(producers, 0);
+    std::vector<std::string> msgs(producers);
+    VerifyMicroBatcher mb(max_batch, std::chrono::microseconds(max_delay_us));
+    std::vector<std::thread> th;
+    for (int p = 0; p < producers; ++p) {
+      th.emplace_back([&, p] {
+        std::vector<std::pair<size_t, std::future<bool>>> futs;
+        for (size_t i = (size_t)p; i < n; i += (size_t)producers) {
+          PublicKey k;
+          std::memcpy(k.ed25519().data(), pk + 32 * i, 32);
+          Signature s(sig + 64 * i, sig + 64 * i + 64);
+          futs.emplace_back(i, mb.submit(k, s, ByteSlice(msg + msg_off[i], msg_len[i])));
+          if (inter_arrival_us) std::this_thread::sleep_for(std::chrono::microseconds(inter_arrival_us));
+        }
+        try {
+          for (auto& f : futs) verdict[f.first] = f.second.get() ? 1 : 0;
+        } catch (std::exception const& e) {
+          err[p] = 1;
+          msgs[p] = e.what();
+        }
+      });
+    }
+    for (auto& t : th) t.join();
+    for (int p = 0; p < producers; ++p)
+      if (err[p]) {
+        t_err = msgs[p];
+        return SVH_ERR_ENGINE;
+      }
+    if (stats) {
+      auto s = mb.stats();
+      stats->items = s.items;
+      stats->batches = s.batches;
+      stats->flushed_by_size = s.flushedBySize;
+      stats->flushed_by_deadline = s.flushedByDeadline;
+      stats->max_batch = s.maxBatchSeen;
+      std::vector<double> lat = mb.latencies();
+      std::sort(lat.begin(), lat.end());
+      stats->lat_p50_us = lat.empty() ? 0 : lat[lat.size() / 2];
+      stats->lat_p99_us = lat.empty() ? 0 : lat[std::min(lat.size() - 1, (size_t)(lat.size() * 0.99))];
     }
     return SVH_OK;
   } catch (std::exception const& e) {

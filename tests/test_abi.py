@@ -44,6 +44,19 @@ def test_library_exports_every_declared_symbol(lib_path, sv):
     assert set(sv.EXPORTED_SYMBOLS) <= set(_declared_functions())
 
 
+def test_host_library_exports_every_declared_symbol(sv):
+    """libstellar_host.so (C++ PubKeyUtils / SignatureChecker / micro-batcher
+    mirror) exports every svh_* entry point include/stellar_host.h declares."""
+    if not os.path.exists(sv.HOSTLIB_PATH):
+        subprocess.run(["make", "-s", "-j4"], cwd=os.path.join(REPO, "stellar-core_amd"), check=True)
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(REPO, "include", "stellar_host.h")).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(svh_[a-z0-9_]+)\s*\(", src)) - {"svh_batch_verify_fn"})
+    assert "svh_mb_run" in names and "svh_check_txset" in names
+    lib = ctypes.CDLL(sv.HOSTLIB_PATH)
+    for name in names:
+        assert hasattr(lib, name), name
+
+
 def test_code_object_is_gfx950_only(lib_path):
     blob = open(lib_path, "rb").read()
     targets = set(re.findall(rb"amdgcn-amd-amdhsa-[-a-z]*(gfx[0-9a-z]+)", blob))

@@ -1,0 +1,290 @@
+#!/usr/bin/env python3
+"""Secondary BASELINE.json configs on one MI355X (developer/report tool; the
+headline line is bench.py = config 2).  Prints one JSON object.
+
+  config1  100k random signatures over 32-byte hashes, and the reference's own
+           benchmark shape (10k keys x 256-byte messages, SecretKey.cpp:182-234):
+           GPU via the host API (PCIe-inclusive) and device API (kernel only),
+           libsodium raw on 1 and all host threads, and the verifySig-equivalent
+           path (C++ PubKeyUtils mirror: BLAKE2b key + cache + mutex) with
+           libsodium behind it.
+  config3  synthetic 5000-tx ledger, 1-20 ED25519 signers per tx (+ HASH_X,
+           PRE_AUTH_TX, signed-payload signers, wrong-key colliding hints):
+           C++ SignatureChecker mirror with the one-batch GPU pre-pass vs the
+           same checker with per-signature libsodium (the reference's path);
+           outcomes compared with an independent Python replay.
+  config5  catchup scale: 64 x 2^20 signatures (the libsodium-pinned 1M set
+           tiled 64x, cache bypassed) in one device-resident batch.
+"""
+import argparse
+import ctypes
+import hashlib
+import importlib
+import json
+import os
+import struct
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+SODIUM = "/opt/conda/lib/libsodium.so.23"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def threads():
+    return max(1, min(64, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)))
+
+
+class Env:
+    def __init__(self):
+        import torch
+        self.torch = torch
+        self.sv = importlib.import_module("stellar-core_amd")
+        self.dev = torch.device("cuda", 0)
+        self.stream = torch.cuda.current_stream(self.dev).cuda_stream
+        self.base = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+        self.base.cpubase_run.restype = ctypes.c_double
+        self.base.cpubase_run.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_uint32, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        self.have_sodium = os.path.exists(SODIUM)
+        self.sodium = ctypes.CDLL(SODIUM) if self.have_sodium else None
+        if self.sodium is not None:
+            assert self.sodium.sodium_init() >= 0
+        self.host = ctypes.CDLL(self.sv.HOSTLIB_PATH)
+        self.host.svh_last_error_string.restype = ctypes.c_char_p
+        self.host.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+
+    def gpu_sign(self, seeds, msgs):
+        t = self.torch
+        n = seeds.shape[0]
+        ts = t.from_numpy(np.array(seeds, copy=True)).to(self.dev)
+        tm = t.from_numpy(np.array(msgs, copy=True)).to(self.dev)
+        pk = t.empty((n, 32), dtype=t.uint8, device=self.dev)
+        sg = t.empty((n, 64), dtype=t.uint8, device=self.dev)
+        self.sv.sign_device(0, ts.data_ptr(), tm.data_ptr(), n, pk.data_ptr(), sg.data_ptr(), self.stream)
+        t.cuda.synchronize(self.dev)
+        return pk, sg, tm
+
+    def sodium_sign(self, seed, msg):
+        pk = ctypes.create_string_buffer(32)
+        sk = ctypes.create_string_buffer(64)
+        self.sodium.crypto_sign_seed_keypair(pk, sk, seed)
+        s = ctypes.create_string_buffer(64)
+        self.sodium.crypto_sign_detached(s, None, msg, ctypes.c_ulonglong(len(msg)), sk)
+        return pk.raw, s.raw
+
+    def cpu_rate(self, pk, sig, msg, mlen, nthreads):
+        n = pk.shape[0]
+        out = np.zeros(n, np.uint8)
+        pk, sig, msg = (np.ascontiguousarray(x) for x in (pk, sig, msg))
+        dt = self.base.cpubase_run(SODIUM.encode() if self.have_sodium else None, pk.ctypes.data, sig.ctypes.data,
+                                   msg.ctypes.data, mlen, n, nthreads, out.ctypes.data)
+        return n / dt, out
+
+
+def host_api_rate(env, pk, sig, msg, mlen, reps=3):
+    sv = env.sv
+    sv.verify_fixed(pk[:1024], sig[:1024], msg[:1024 * mlen].reshape(-1), mlen)
+    best = 1e9
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = sv.verify_fixed(pk, sig, msg.reshape(-1), mlen)
+        best = min(best, time.perf_counter() - t0)
+    return pk.shape[0] / best, out
+
+
+def device_rate(env, tpk, tsig, tmsg, n, mlen, reps=5):
+    t, sv = env.torch, env.sv
+    tv = t.zeros(n, dtype=t.uint8, device=env.dev)
+    sv.verify_device(0, tpk.data_ptr(), tsig.data_ptr(), tmsg.data_ptr(), n, tv.data_ptr(), 0, env.stream,
+                     fixed_msg_len=mlen)
+    t.cuda.synchronize(env.dev)
+    sv.kernel_time_reset()
+    sv.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sv.verify_device(0, tpk.data_ptr(), tsig.data_ptr(), tmsg.data_ptr(), n, tv.data_ptr(), 0, env.stream,
+                         fixed_msg_len=mlen)
+    sv.synchronize(0)
+    t.cuda.synchronize(env.dev)
+    wall = (time.perf_counter() - t0) / reps
+    sv.timing_enable(False)
+    ms, la, _ = sv.kernel_time(0)
+    return n / wall, n / (ms / la * 1e-3), tv.cpu().numpy()
+
+
+def verifysig_equivalent_rate(env, pk, sig, msg, mlen, nthreads):
+    """C++ PubKeyUtils mirror (BLAKE2b key, cache, mutex) with libsodium behind it."""
+    if not env.have_sodium:
+        return None
+    base = env.base
+    base.cpubase_set_sodium.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    assert base.cpubase_set_sodium(SODIUM.encode(), nthreads) == 0
+    env.host.svh_set_test_verifier(ctypes.cast(base.cpubase_sodium_batch, ctypes.c_void_p))
+    env.host.svh_cache_clear()
+    n = pk.shape[0]
+    off = (np.arange(n, dtype=np.uint64) * mlen)
+    ln = np.full(n, mlen, np.uint32)
+    out = np.zeros(n, np.uint8)
+    pk, sig, msg = (np.ascontiguousarray(x) for x in (pk, sig, msg))
+    t0 = time.perf_counter()
+    rc = env.host.svh_verify_sig_batch(ctypes.c_void_p(pk.ctypes.data), ctypes.c_void_p(sig.ctypes.data), None,
+                                       ctypes.c_void_p(msg.ctypes.data), ctypes.c_void_p(off.ctypes.data),
+                                       ctypes.c_void_p(ln.ctypes.data), ctypes.c_size_t(n),
+                                       ctypes.c_void_p(out.ctypes.data))
+    dt = time.perf_counter() - t0
+    env.host.svh_set_test_verifier(None)
+    env.host.svh_cache_clear()
+    assert rc == 0
+    return n / dt
+
+
+def config1(env):
+    res = {}
+    T = threads()
+    rng = np.random.default_rng(1)
+    n = 100_000
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    tpk, tsig, tm = env.gpu_sign(seeds, msgs)
+    pk, sig = tpk.cpu().numpy(), tsig.cpu().numpy()
+    host_rate, out_h = host_api_rate(env, pk, sig, msgs, 32)
+    wall_rate, kern_rate, out_d = device_rate(env, tpk, tsig, tm, n, 32)
+    cpu1, o1 = env.cpu_rate(pk[:10000], sig[:10000], msgs[:10000], 32, 1)
+    cpuT, oT = env.cpu_rate(pk, sig, msgs, 32, T)
+    vse1 = verifysig_equivalent_rate(env, pk[:10000], sig[:10000], msgs[:10000], 32, 1)
+    res["100k_x_32B"] = {
+        "gpu_host_api_verifies_per_s": host_rate, "gpu_device_api_verifies_per_s": wall_rate,
+        "gpu_kernel_verifies_per_s": kern_rate, "cpu_libsodium_1thread": cpu1,
+        "cpu_libsodium_threads": cpuT, "cpu_threads": T, "cpu_verifysig_equivalent_1thread": vse1,
+        "all_valid": bool(out_h.all() and out_d.all() and o1.all() and oT.all()),
+    }
+    if env.have_sodium:
+        k = 10_000
+        pks, sigs, ms = [], [], []
+        for i in range(k):
+            m = hashlib.shake_256(b"REF256" + struct.pack("<Q", i)).digest(256)
+            p, s = env.sodium_sign(hashlib.sha256(b"REFKEY" + struct.pack("<Q", i)).digest(), m)
+            pks.append(p); sigs.append(s); ms.append(m)
+        pk2 = np.frombuffer(b"".join(pks), np.uint8).reshape(k, 32)
+        sg2 = np.frombuffer(b"".join(sigs), np.uint8).reshape(k, 64)
+        m2 = np.frombuffer(b"".join(ms), np.uint8).reshape(k, 256)
+        hr, oh = host_api_rate(env, pk2, sg2, m2, 256)
+        c1, oc1 = env.cpu_rate(pk2, sg2, m2, 256, 1)
+        cT, ocT = env.cpu_rate(pk2, sg2, m2, 256, T)
+        v1 = verifysig_equivalent_rate(env, pk2, sg2, m2, 256, 1)
+        res["ref_shape_10k_x_256B"] = {
+            "gpu_host_api_verifies_per_s": hr, "cpu_libsodium_1thread": c1, "cpu_libsodium_threads": cT,
+            "cpu_threads": T, "cpu_verifysig_equivalent_1thread": v1,
+            "all_valid": bool(oh.all() and oc1.all() and ocT.all()),
+        }
+    return res
+
+
+def config3(env, n_tx=5000):
+    import txset_gen as tg
+    t0 = time.perf_counter()
+
+    def gpu_sign_fn(reqs):
+        seeds = np.frombuffer(b"".join(r[0] for r in reqs), np.uint8).reshape(-1, 32)
+        msgs = np.frombuffer(b"".join(r[1] for r in reqs), np.uint8).reshape(-1, 32)
+        tpk, tsig, _ = env.gpu_sign(seeds, msgs)
+        pk, sg = tpk.cpu().numpy(), tsig.cpu().numpy()
+        return [(pk[i].tobytes(), sg[i].tobytes()) for i in range(len(reqs))]
+
+    def var_sign_fn(reqs):
+        return [env.sodium_sign(s, m) for s, m in reqs]
+
+    txs = tg.generate(n_tx, gpu_sign_fn, seed=2025)
+    if env.have_sodium:
+        tg.add_payload_signatures(txs, var_sign_fn)
+    gen_s = time.perf_counter() - t0
+    T, S, G = tg.to_ctypes(txs)
+    nsig = sum(len(t["sigs"]) for t in txs)
+
+    def run(prefetch):
+        ok = np.zeros(n_tx, np.uint8)
+        used = np.zeros(n_tx, np.uint8)
+        pairs = ctypes.c_uint64()
+        env.host.svh_cache_clear()
+        t1 = time.perf_counter()
+        rc = env.host.svh_check_txset(T, ctypes.c_size_t(n_tx), S, G, prefetch, ok.ctypes.data_as(ctypes.c_void_p),
+                                      used.ctypes.data_as(ctypes.c_void_p), ctypes.byref(pairs))
+        dt = time.perf_counter() - t1
+        assert rc == 0, env.host.svh_last_error_string()
+        return ok, used, dt, pairs.value
+
+    ok_g, used_g, dt_g, pairs = run(1)
+    out = {"txs": n_tx, "decorated_signatures": nsig, "prefetched_pairs": pairs, "generate_s": gen_s,
+           "gpu_prepass_checker_s": dt_g, "gpu_prepass_txs_per_s": n_tx / dt_g}
+    if env.have_sodium:
+        base = env.base
+        base.cpubase_set_sodium.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        assert base.cpubase_set_sodium(SODIUM.encode(), 1) == 0
+        env.host.svh_set_test_verifier(ctypes.cast(base.cpubase_sodium_batch, ctypes.c_void_p))
+        ok_c, used_c, dt_c, _ = run(0)  # reference path: per-signature libsodium, one thread
+        env.host.svh_set_test_verifier(None)
+        env.host.svh_cache_clear()
+        so = env.sodium
+
+        def verify(pk, sig, msg):
+            return so.crypto_sign_verify_detached(sig, msg, ctypes.c_ulonglong(len(msg)), pk) == 0
+
+        want_ok, want_used = tg.replay(txs, verify)
+        out.update({
+            "cpu_reference_checker_s": dt_c, "cpu_reference_txs_per_s": n_tx / dt_c,
+            "speedup": dt_c / dt_g,
+            "outcomes_match_python_replay": bool((ok_g == want_ok).all() and (used_g == want_used).all()
+                                                 and (ok_c == want_ok).all() and (used_c == want_used).all()),
+            "txs_ok": int(want_ok.sum()), "txs_all_sigs_used": int(want_used.sum()),
+        })
+    return out
+
+
+def config5(env, tiles=64):
+    t = env.torch
+    n1 = 1 << 20
+    s = bytearray()
+    m = bytearray()
+    for i in range(n1):
+        p = struct.pack("<Q", i)
+        s += hashlib.sha256(b"SVSEED" + p).digest()
+        m += hashlib.sha256(b"SVMSG" + p).digest()
+    seeds = np.frombuffer(bytes(s), np.uint8).reshape(n1, 32)
+    msgs = np.frombuffer(bytes(m), np.uint8).reshape(n1, 32)
+    tpk, tsig, tm = env.gpu_sign(seeds, msgs)
+    n = n1 * tiles
+    bpk = tpk.repeat(tiles, 1)
+    bsig = tsig.repeat(tiles, 1)
+    bmsg = tm.repeat(tiles, 1)
+    wall, kern, out = device_rate(env, bpk, bsig, bmsg, n, 32, reps=2)
+    return {"signatures": n, "construction": "libsodium-pinned 2^20 dataset tiled %dx on device" % tiles,
+            "device_api_verifies_per_s": wall, "kernel_verifies_per_s": kern, "all_valid": bool(out.all()),
+            "seconds_per_batch": n / wall}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="1,3,5")
+    ap.add_argument("--txs", type=int, default=5000)
+    args = ap.parse_args()
+    env = Env()
+    res = {"device": "MI355X", "cpu_threads": threads()}
+    for c in args.configs.split(","):
+        t0 = time.perf_counter()
+        res["config" + c] = {"1": lambda: config1(env), "3": lambda: config3(env, args.txs),
+                             "5": lambda: config5(env)}[c]()
+        log("config %s done in %.1fs" % (c, time.perf_counter() - t0))
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
