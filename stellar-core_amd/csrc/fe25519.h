@@ -88,8 +88,22 @@ SV_HD void fe_weak(fe& h) {
 
 // Sequential carry of 64-bit column sums into a carried fe (R).
 // Order interleaves two chains for ILP (0->1->2->3->4 and 4->5->...->9->0).
+#ifndef SV_CARRY_SINGLE
+#define SV_CARRY_SINGLE 1
+#endif
 SV_HD void fe_carry_wide(fe& out, uint64_t h[10]) {
   uint64_t c;
+#if SV_CARRY_SINGLE
+  // one chain 0->1->...->9->0->1: 11 steps (VALU back-to-back dependent
+  // issue is free on CDNA, so the 12-step two-chain form buys no ILP)
+  SV_UNROLL for (int i = 0; i < 9; ++i) {
+    c = h[i] >> fe_width(i); h[i + 1] += c; h[i] &= fe_mask(i);
+  }
+  c = h[9] >> 25; h[0] += c * 19u; h[9] &= SV_M25;
+  c = h[0] >> 26; h[1] += c; h[0] &= SV_M26;
+  SV_UNROLL for (int i = 0; i < 10; ++i) out.v[i] = (uint32_t)h[i];
+  return;
+#endif
   c = h[0] >> 26; h[1] += c; h[0] &= SV_M26;
   c = h[4] >> 26; h[5] += c; h[4] &= SV_M26;
   c = h[1] >> 25; h[2] += c; h[1] &= SV_M25;
@@ -111,15 +125,18 @@ SV_HD void fe_carry_wide(fe& out, uint64_t h[10]) {
 // 64x32-bit products (2 v_mad_u64_u32 + 2 v_mov each).  The carry-out SGPR
 // pair is architecturally required on gfx950 (no `null` sdst); vcc is used
 // and never read.
+#ifndef SV_MAD_ASM
+#define SV_MAD_ASM 1
+#endif
 SV_HD void sv_mad_init(uint64_t& acc, uint32_t a, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
   asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "vcc");
 #else
   acc = (uint64_t)a * b;
 #endif
 }
 SV_HD void sv_mad(uint64_t& acc, uint32_t a, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
   asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
 #else
   acc += (uint64_t)a * b;
@@ -147,6 +164,9 @@ SV_HD void fe_mul_cols(uint64_t h[10], const fe& f, const fe& g) {
   }
 }
 
+#ifndef SV_SQ_ASM
+#define SV_SQ_ASM 0
+#endif
 // Column sums of f^2 (DBL: 2 f^2), using the symmetry f_i f_j = f_j f_i.
 template <bool DBL>
 SV_HD void fe_sq_cols(uint64_t h[10], const fe& f) {
@@ -156,8 +176,15 @@ SV_HD void fe_sq_cols(uint64_t h[10], const fe& f) {
       const int sh = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + (DBL ? 1 : 0);
       const uint32_t a = f.v[i] << sh;
       const uint32_t b = (k >= 10) ? 19u * f.v[j] : f.v[j];
-      if (i == 0) sv_mad_init(h[k], a, b);  // i == 0 opens every column
+#if SV_SQ_ASM
+      if (i == 0) sv_mad_init(h[k], a, b);
       else sv_mad(h[k >= 10 ? k - 10 : k], a, b);
+#else
+      // plain C here: squaring operands are never phi-merged, so LLVM keeps
+      // them 32-bit, and compiler-emitted mads need no hazard s_nops
+      if (i == 0) h[k] = (uint64_t)a * b;  // i == 0 opens every column
+      else h[k >= 10 ? k - 10 : k] += (uint64_t)a * b;
+#endif
     }
   }
 }

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Developer tool: GPU A/B timing of verify-library variants (built by
+tools/build_variants.sh).  One 2^20 fixed-32B batch signed on the GPU (1/8 of
+the rows corrupted); every variant must reproduce the baseline's verdicts;
+prints kernel ms per launch (median over interleaved rounds) per variant."""
+import ctypes
+import glob
+import os
+import sys
+
+import torch  # noqa: F401  (load torch's HIP runtime first)
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+paths = sys.argv[1:] or sorted(glob.glob(os.path.join(REPO, "variants", "libsv_*.so")))
+libs = {}
+for p in paths:
+    lib = ctypes.CDLL(p, mode=os.RTLD_LOCAL)
+    lib.sv_kernel_time.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
+                                   ctypes.POINTER(ctypes.c_uint64)]
+    assert lib.sv_init() == 0
+    libs[os.path.basename(p)] = lib
+
+dev = torch.device("cuda", 0)
+n = 1 << 20
+g = torch.Generator(device="cpu").manual_seed(5)
+seeds = torch.randint(0, 256, (n, 32), dtype=torch.uint8, generator=g).to(dev)
+msgs = torch.randint(0, 256, (n, 32), dtype=torch.uint8, generator=g).to(dev)
+pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+first = next(iter(libs.values()))
+vp = ctypes.c_void_p
+assert first.sv_ed25519_sign_device(0, vp(seeds.data_ptr()), vp(msgs.data_ptr()), ctypes.c_size_t(n),
+                                    vp(pk.data_ptr()), vp(sig.data_ptr()), None) == 0
+first.sv_device_synchronize(0)
+sig[::8, 3] ^= 1
+torch.cuda.synchronize()
+want = None
+res = {k: [] for k in libs}
+for rnd in range(4):
+    for name, lib in libs.items():
+        out = torch.zeros(n, dtype=torch.uint8, device=dev)
+        lib.sv_timing_enable(1)
+        lib.sv_kernel_time_reset()
+        for _ in range(3):
+            assert lib.sv_ed25519_verify_device(0, vp(pk.data_ptr()), vp(sig.data_ptr()), vp(msgs.data_ptr()), None,
+                                                None, 32, ctypes.c_size_t(n), vp(out.data_ptr()), None, None) == 0
+        lib.sv_device_synchronize(0)
+        ms, la, sg = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint64()
+        lib.sv_kernel_time(0, ctypes.byref(ms), ctypes.byref(la), ctypes.byref(sg))
+        lib.sv_timing_enable(0)
+        o = out.cpu().numpy()
+        if want is None:
+            want = o
+            assert o.sum() == n - n // 8, o.sum()
+        assert (o == want).all(), name + " verdict mismatch"
+        res[name].append(ms.value / la.value)
+        print("round %d %-28s %.3f ms" % (rnd, name, ms.value / la.value), flush=True)
+for name, v in res.items():
+    print("%-28s median %.3f ms per 2^20  (%.3e verifies/s)" % (name, float(np.median(v)), n / (np.median(v) * 1e-3)))

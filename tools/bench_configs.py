@@ -13,6 +13,10 @@ headline line is bench.py = config 2).  Prints one JSON object.
            C++ SignatureChecker mirror with the one-batch GPU pre-pass vs the
            same checker with per-signature libsodium (the reference's path);
            outcomes compared with an independent Python replay.
+  configmb SCP/overlay flood through the VerifyMicroBatcher:
+           8 producer threads submit 200k envelope-sized (~180 B) messages;
+           GPU engine behind verifySigBatch vs libsodium behind it; throughput
+           and submit->verdict latency p50/p99.
   config5  catchup scale: 64 x 2^20 signatures (the libsodium-pinned 1M set
            tiled 64x, cache bypassed) in one device-resident batch.
 """
@@ -61,6 +65,8 @@ class Env:
         self.host = ctypes.CDLL(self.sv.HOSTLIB_PATH)
         self.host.svh_last_error_string.restype = ctypes.c_char_p
         self.host.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+        env_host_mb = self.host.svh_mb_run
+        env_host_mb.restype = ctypes.c_int
 
     def gpu_sign(self, seeds, msgs):
         t = self.torch
@@ -249,6 +255,71 @@ def config3(env, n_tx=5000):
     return out
 
 
+class MbStats(ctypes.Structure):
+    _fields_ = [("items", ctypes.c_uint64), ("batches", ctypes.c_uint64), ("flushed_by_size", ctypes.c_uint64),
+                ("flushed_by_deadline", ctypes.c_uint64), ("max_batch", ctypes.c_uint64),
+                ("lat_p50_us", ctypes.c_double), ("lat_p99_us", ctypes.c_double)]
+
+
+def configmb(env, n=200_000, producers=8):
+    rng = np.random.default_rng(9)
+    lens = rng.integers(120, 240, n).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    msg = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    nk = 64  # validator-set sized key population
+    pks, sks = [], []
+    for i in range(nk):
+        pk = ctypes.create_string_buffer(32)
+        sk = ctypes.create_string_buffer(64)
+        if env.have_sodium:
+            env.sodium.crypto_sign_seed_keypair(pk, sk, hashlib.sha256(b"VAL" + struct.pack("<Q", i)).digest())
+        pks.append(pk.raw); sks.append(sk.raw)
+    if not env.have_sodium:
+        return {"skipped": "libsodium absent"}
+    kid = rng.integers(0, nk, n)
+    sig = np.zeros((n, 64), np.uint8)
+    s = ctypes.create_string_buffer(64)
+    for i in range(n):
+        o = int(off[i])
+        env.sodium.crypto_sign_detached(s, None, msg[o:o + int(lens[i])].tobytes(), ctypes.c_ulonglong(int(lens[i])),
+                                        sks[kid[i]])
+        sig[i] = np.frombuffer(s.raw, np.uint8)
+    sig[::97, 5] ^= 1  # some forgeries
+    pk = np.ascontiguousarray(np.frombuffer(b"".join(pks), np.uint8).reshape(nk, 32)[kid])
+    want = np.ones(n, np.uint8)
+    want[::97] = 0
+    vp = ctypes.c_void_p
+
+    def run(max_batch, max_delay_us):
+        out = np.zeros(n, np.uint8)
+        st = MbStats()
+        env.host.svh_cache_clear()
+        t0 = time.perf_counter()
+        rc = env.host.svh_mb_run(vp(pk.ctypes.data), vp(sig.ctypes.data), vp(msg.ctypes.data), vp(off.ctypes.data),
+                                 vp(lens.ctypes.data), ctypes.c_size_t(n), producers, ctypes.c_uint32(max_batch),
+                                 ctypes.c_uint32(max_delay_us), ctypes.c_uint32(0), vp(out.ctypes.data),
+                                 ctypes.byref(st))
+        dt = time.perf_counter() - t0
+        assert rc == 0, env.host.svh_last_error_string()
+        return {"verifies_per_s": n / dt, "batches": st.batches, "flushed_by_size": st.flushed_by_size,
+                "flushed_by_deadline": st.flushed_by_deadline, "max_batch_seen": st.max_batch,
+                "lat_p50_us": st.lat_p50_us, "lat_p99_us": st.lat_p99_us,
+                "verdicts_match": bool((out == want).all())}
+
+    res = {"messages": n, "producers": producers, "gpu": {}}
+    for mbatch in (1024, 8192, 65536):
+        res["gpu"]["max_batch_%d" % mbatch] = run(mbatch, 2000)
+    base = env.base
+    base.cpubase_set_sodium.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    assert base.cpubase_set_sodium(SODIUM.encode(), 1) == 0
+    env.host.svh_set_test_verifier(ctypes.cast(base.cpubase_sodium_batch, ctypes.c_void_p))
+    res["cpu_libsodium_1thread_batch_1024"] = run(1024, 2000)
+    env.host.svh_set_test_verifier(None)
+    env.host.svh_cache_clear()
+    return res
+
+
 def config5(env, tiles=64):
     t = env.torch
     n1 = 1 << 20
@@ -273,7 +344,7 @@ def config5(env, tiles=64):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="1,3,5")
+    ap.add_argument("--configs", default="1,3,mb,5")
     ap.add_argument("--txs", type=int, default=5000)
     args = ap.parse_args()
     env = Env()
@@ -281,7 +352,7 @@ def main():
     for c in args.configs.split(","):
         t0 = time.perf_counter()
         res["config" + c] = {"1": lambda: config1(env), "3": lambda: config3(env, args.txs),
-                             "5": lambda: config5(env)}[c]()
+                             "5": lambda: config5(env), "mb": lambda: configmb(env)}[c]()
         log("config %s done in %.1fs" % (c, time.perf_counter() - t0))
     print(json.dumps(res, indent=1))
 
