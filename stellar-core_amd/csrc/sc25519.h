@@ -114,6 +114,21 @@ SV_HD void sc_digits_r256(uint32_t out[8], const uint32_t s[8]) {
   }
 }
 
+// Signed radix-2^16 digits of a scalar < 2^253: 16 digits in [-2^15, 2^15),
+// digit i packed as 16-bit two's complement at bits 16(i%2) of out[i/2].
+SV_HD void sc_digits_r65536(uint32_t out[8], const uint32_t s[8]) {
+  uint32_t carry = 0;
+  SV_UNROLL for (int w = 0; w < 8; ++w) {
+    uint32_t acc = 0;
+    SV_UNROLL for (int k = 0; k < 2; ++k) {
+      const uint32_t v = ((s[w] >> (16 * k)) & 0xffffu) + carry;
+      carry = (v + 0x8000u) >> 16;  // v >= 2^15 (v <= 2^16)
+      acc |= ((v - (carry << 16)) & 0xffffu) << (16 * k);
+    }
+    out[w] = acc;
+  }
+}
+
 // Pop the most significant packed digit: returns it sign-extended and shifts
 // the 256-bit digit string left by `bits`.
 SV_HD int32_t sc_pop_top(uint32_t d[8], int bits) {

@@ -6,7 +6,8 @@
 // wave always hold 64 consecutive signatures (coalesced SoA loads, one
 // ballot word of the verdict bitmap per wave iteration).
 //
-// Memory per workgroup: the 129-entry base-point table (18.6 KiB) in LDS.
+// Memory per workgroup: a 12 KiB LDS stage per wave for the next table_A entry.
+// Per device: the 2^15+1-entry base-point table (4.7 MB, global, L2/MALL-hot).
 // Memory per lane: a 2304 B slot of the HBM workspace: the signature's 9-entry
 // table of multiples of -A (1728 B) + SV_BATCH_K parked projective points.
 // Lane-major: lanes gather different entries (per-lane digits), so keeping
@@ -17,6 +18,9 @@
 #include "verify_core.h"
 
 #define SV_BLOCK 256
+#ifndef SV_STAGE_A
+#define SV_STAGE_A 1  // table_A entries via LDS-DMA prefetch (verify_core.h)
+#endif
 #define SV_WAVES_PER_SIMD 2
 
 struct sv_kparams {
@@ -71,10 +75,17 @@ __device__ __forceinline__ void sv_load_and_hash(const sv_kparams& p, uint64_t i
 // and enter the batch inversion as Z = 1.
 template <int MODE>  // 0: fixed 32-byte messages, 1: variable length, 2: fixed other length
 __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_kernel(sv_kparams p) {
+#if SV_B_BITS == 8
   __shared__ sv_u4 s_btab[SV_BTAB_ENTRIES * (SV_BTAB_STRIDE / 4)];
   sv_load_btab_lds(s_btab, p.btab);
+  const sv_u4* btab = s_btab;
+#else
+  const sv_u4* btab = p.btab;  // 4.7 MB, L2/MALL-resident
+#endif
+  __shared__ sv_u4 s_stage[SV_BLOCK / 64][SV_STAGE_QUADS];  // per-wave table_A entry stage
 
   const uint32_t lane = threadIdx.x & 63u;
+  sv_u4* stage = s_stage[threadIdx.x >> 6];
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // lane-major workspace slot: table_A (1728 B) + K pending points
   sv_u4* slot = p.ws + gtid * SV_SLOT_QUADS;
@@ -93,7 +104,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_kernel(
       uint32_t A[8], S[8], hram[16];
       sv_load_and_hash<MODE>(p, ii, A, S, hram);
       ge_p3 P;
-      const bool ok = sv_verify_pre(P, A, p.sig + 4 * ii, S, hram, slot, 1, s_btab);
+      const bool ok = sv_verify_pre<SV_STAGE_A>(P, A, p.sig + 4 * ii, S, hram, slot, 1, btab, stage);
       okmask |= (ok ? 1u : 0u) << k;
       sv_store_fe3(pend + k * SV_PEND_QUADS, 1, P.X);
       sv_store_fe3(pend + k * SV_PEND_QUADS + 3, 1, P.Y);
@@ -141,8 +152,12 @@ struct sv_sparams {
 };
 
 __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_sign_kernel(sv_sparams p) {
+#if SV_B_BITS == 8
   __shared__ sv_u4 s_btab[SV_BTAB_ENTRIES * (SV_BTAB_STRIDE / 4)];
   sv_load_btab_lds(s_btab, p.btab);
+#else
+  const sv_u4* s_btab = p.btab;
+#endif
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   sv_u4* slot = p.ws + gtid * SV_SLOT_QUADS;
@@ -172,7 +187,7 @@ size_t sv_btab_bytes(void) { return (size_t)SV_BTAB_DWORDS * 4; }
 int sv_block_threads(void) { return SV_BLOCK; }
 
 hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s) {
-  hipLaunchKernelGGL(sv_btab_init_kernel, dim3(1), dim3(192), 0, s, d_btab);
+  hipLaunchKernelGGL(sv_btab_init_kernel, dim3((SV_BTAB_ENTRIES + 191) / 192), dim3(192), 0, s, d_btab);
   return hipGetLastError();
 }
 

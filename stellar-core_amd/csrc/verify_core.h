@@ -14,12 +14,13 @@
 //
 // Step (7) schedule (wave-uniform, no per-lane branches):
 //   64 windows of 4 bits.  Per window: 4 doublings; add table_A[d_A] with
-//   d_A in [-8, 7] (signed radix 16 of h); on even windows also add
-//   table_B[d_B], d_B in [-128, 127] (signed radix 256 of S).
+//   d_A in [-8, 8] (signed radix 16 of h); on every 4th window also add
+//   table_B[d_B], d_B in [-2^15, 2^15] (signed radix 2^16 of S; SV_B_BITS).
 //   table_A = {0..8}·(-A) in cached form, built per lane into an HBM workspace
 //   slot (1728 B/lane, lane-major so a lane's entry is 192 contiguous bytes;
-//   too big for LDS at >= 2 waves/SIMD);
-//   table_B = {0..128}·B in affine precomp form, shared by the workgroup in LDS.
+//   too big for LDS at >= 2 waves/SIMD), each window's entry prefetched into
+//   LDS by DMA while the window doubles;
+//   table_B = {0..2^15}·B in affine precomp form, one global copy per device.
 //   Zero digits add the identity entry, so every lane does identical work.
 #pragma once
 
@@ -33,8 +34,16 @@ struct __attribute__((aligned(16))) sv_u4 {
 
 // Every table field element is padded to 12 dwords (3 quads) so a negative
 // digit's (Y+X) <-> (Y-X) swap is an address choice at load time.
-// B-table (LDS / global): entry e = 36 dwords: ypx[12] ymx[12] xy2d[12]
-#define SV_BTAB_ENTRIES 129
+// B-table: entry e = e·B as 36 dwords: ypx[12] ymx[12] xy2d[12].
+//   SV_B_BITS 16 (default): signed radix-2^16 digits of S, one B addition
+//     every 4th window (16 per signature), 2^15 + 1 entries = 4.7 MB read from
+//     global memory (L2/MALL-resident).
+//   SV_B_BITS 8: signed radix-256 digits, every other window (32 additions),
+//     129 entries = 18.6 KB staged into LDS per workgroup.
+#ifndef SV_B_BITS
+#define SV_B_BITS 16
+#endif
+#define SV_BTAB_ENTRIES ((1 << (SV_B_BITS - 1)) + 1)
 #define SV_BTAB_STRIDE 36
 #define SV_BTAB_DWORDS (SV_BTAB_ENTRIES * SV_BTAB_STRIDE)
 // A-table (HBM workspace): 9 entries x 12 quads: YpX YmX Z T2d (3 quads each)
@@ -114,37 +123,90 @@ SV_COLD void sv_build_atab(sv_u4* slot, int qstride, const ge_p3& negA) {
 // Step machine: per window w (64 of them, MSB first) run steps
 //   s = 0..3  doubling, s = 4  add table_A[d_A], s = 5 (even w) add table_B[d_B]
 // with one code instance of each step kind; every branch is wave-uniform.
+// Per-wave LDS stage for the next table_A entry: [12 quads][64 lanes] x 16 B.
+#define SV_STAGE_QUADS (SV_ATAB_QUADS * 64)
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// Device: the window's table_A entry is fetched by LDS-DMA (global_load_lds,
+// no VGPR destination) when the window starts, so the HBM/L2 latency hides
+// behind the window's 4 doublings instead of stalling the addition.  The
+// +/- swap of (Y+X, Y-X) is done by the per-lane SOURCE address; the LDS image
+// is lane-linear (a DMA writes wave-uniform base + lane x 16 B).
+SV_HD void sv_stage_aentry(sv_u4* stage, const sv_u4* slot, int qstride, int32_t d) {
+  const bool neg = d < 0;
+  const sv_u4* e = slot + (neg ? -d : d) * SV_ATAB_QUADS * qstride;
+  const sv_u4* ea = e + (neg ? 3 : 0) * qstride;
+  const sv_u4* eb = e + (neg ? 0 : 3) * qstride;
+  // the previous window's LDS reads of the stage have retired before the
+  // DMA may overwrite it
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  SV_UNROLL for (int q = 0; q < SV_ATAB_QUADS; ++q) {
+    const sv_u4* src = q < 3 ? ea + q * qstride : (q < 6 ? eb + (q - 3) * qstride : e + q * qstride);
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(stage + q * 64),
+                                     16, 0, 0);
+  }
+}
+// hipcc does not count LDS-DMA completion before LDS reads: wait explicitly
+// (no other vector-memory op is in flight inside the window).
+SV_HD void sv_stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+#endif
+
+// STAGED (device only): table_A entries arrive through the wave's LDS stage.
+template <bool STAGED = false>
 SV_HD void sv_double_scalarmult(ge_p3& P, const ge_p3& negA, const uint32_t h[8], const uint32_t S[8],
-                                sv_u4* slot, int qstride, const sv_u4* btab) {
+                                sv_u4* slot, int qstride, const sv_u4* btab, sv_u4* stage = nullptr) {
   sv_build_atab(slot, qstride, negA);
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (STAGED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // table stores before the DMA reads
+#endif
 
   uint32_t da[8], db[8];
   sc_digits_r16(da, h);
+#if SV_B_BITS == 16
+  sc_digits_r65536(db, S);
+#else
   sc_digits_r256(db, S);
+#endif
 
   fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
   ge_p1p1 Q;
   SV_NOUNROLL for (int w = 63; w >= 0; --w) {
-    const int nsteps = (w & 1) ? 5 : 6;
+    const int nsteps = (w & (SV_B_BITS / 4 - 1)) ? 5 : 6;
+    const int32_t dA = sc_pop_top(da, 4);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (STAGED) sv_stage_aentry(stage, slot, qstride, dA);
+#endif
     SV_NOUNROLL for (int s = 0; s < nsteps; ++s) {
       if (s < 4) {
         ge_dbl(Q, P.X, P.Y, P.Z);
       } else {
-        // (loading the table_A entry earlier, before the doublings, spills:
-        // a doubling leaves no room for 40 more live VGPRs at 2 waves/SIMD)
+        // (loading the table_A entry into VGPRs before the doublings spills:
+        // a doubling leaves no room for 40 more live VGPRs at 2 waves/SIMD;
+        // the staged path parks it in LDS instead)
         fe qa, qb, qz, qt;
         bool neg;
         const bool zone = s == 5;
         if (!zone) {
-          const int32_t d = sc_pop_top(da, 4);
-          neg = d < 0;
-          const sv_u4* e = slot + (neg ? -d : d) * SV_ATAB_QUADS * qstride;
-          sv_load_fe3(qa, e + (neg ? 3 : 0) * qstride, qstride);
-          sv_load_fe3(qb, e + (neg ? 0 : 3) * qstride, qstride);
-          sv_load_fe3(qz, e + 6 * qstride, qstride);
-          sv_load_fe3(qt, e + 9 * qstride, qstride);
+          neg = dA < 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+          if (STAGED) {
+            sv_stage_wait();
+            const sv_u4* st = stage + __lane_id();
+            sv_load_fe3(qa, st, 64);
+            sv_load_fe3(qb, st + 3 * 64, 64);
+            sv_load_fe3(qz, st + 6 * 64, 64);
+            sv_load_fe3(qt, st + 9 * 64, 64);
+          } else
+#endif
+          {
+            const sv_u4* e = slot + (neg ? -dA : dA) * SV_ATAB_QUADS * qstride;
+            sv_load_fe3(qa, e + (neg ? 3 : 0) * qstride, qstride);
+            sv_load_fe3(qb, e + (neg ? 0 : 3) * qstride, qstride);
+            sv_load_fe3(qz, e + 6 * qstride, qstride);
+            sv_load_fe3(qt, e + 9 * qstride, qstride);
+          }
         } else {
-          const int32_t d = sc_pop_top(db, 8);
+          const int32_t d = sc_pop_top(db, SV_B_BITS);
           neg = d < 0;
           const sv_u4* e = btab + (neg ? -d : d) * (SV_BTAB_STRIDE / 4);
           sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
@@ -172,8 +234,10 @@ SV_HD void sv_double_scalarmult_encode(uint32_t enc[8], const ge_p3& negA, const
 // lane rejected by (1)-(5), P.Z is set to 1 so that a batch inversion over
 // several signatures (sv_finalize_batch) can never be poisoned by a garbage
 // point; its encoding is irrelevant to its (already false) verdict.
+template <bool STAGED = false>
 SV_HD bool sv_verify_pre(ge_p3& P, const uint32_t A[8], const sv_u4* Rp, const uint32_t S[8],
-                         const uint32_t hram[16], sv_u4* slot, int qstride, const sv_u4* btab) {
+                         const uint32_t hram[16], sv_u4* slot, int qstride, const sv_u4* btab,
+                         sv_u4* stage = nullptr) {
   bool ok;
   {
     uint32_t R[8];
@@ -192,7 +256,7 @@ SV_HD bool sv_verify_pre(ge_p3& P, const uint32_t A[8], const sv_u4* Rp, const u
   uint32_t Sc[8];
   SV_UNROLL for (int i = 0; i < 8; ++i) Sc[i] = S[i];
   Sc[7] &= 0x0fffffffu;
-  sv_double_scalarmult(P, negA, h, Sc, slot, qstride, btab);
+  sv_double_scalarmult<STAGED>(P, negA, h, Sc, slot, qstride, btab, stage);
   if (!ok) fe_1(P.Z);
   return ok;
 }
@@ -235,7 +299,7 @@ SV_HD void fe_batch_invert(fe zi[K], const fe z[K]) {
 }
 
 // Base-point table entry e = e·B in affine precomp form (used at init).
-// Computes e·B by double-and-add from B (e <= 128) and normalises.
+// Computes e·B by binary double-and-add from B (e <= 2^15) and normalises.
 SV_HD void sv_btab_entry(uint32_t out[SV_BTAB_STRIDE], int e) {
   const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                             0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
@@ -246,9 +310,13 @@ SV_HD void sv_btab_entry(uint32_t out[SV_BTAB_STRIDE], int e) {
   // acc = identity
   fe_0(acc.X); fe_1(acc.Y); fe_1(acc.Z); fe_0(acc.T);
   ge_p1p1 Q;
-  for (int i = 0; i < e; ++i) {
-    ge_add_preswapped(Q, acc, bc.YpX, bc.YmX, bc.Z, bc.T2d, false, false);
+  for (int bit = SV_B_BITS - 1; bit >= 0; --bit) {
+    ge_dbl(Q, acc.X, acc.Y, acc.Z);
     ge_p1p1_to_p3(acc, Q);
+    if ((e >> bit) & 1) {
+      ge_add_preswapped(Q, acc, bc.YpX, bc.YmX, bc.Z, bc.T2d, false, false);
+      ge_p1p1_to_p3(acc, Q);
+    }
   }
   fe zi, x, y, xy, d2, ypx, ymx, xy2d;
   fe_invert(zi, acc.Z);

@@ -98,7 +98,7 @@ class Env:
 
 def host_api_rate(env, pk, sig, msg, mlen, reps=3):
     sv = env.sv
-    sv.verify_fixed(pk[:1024], sig[:1024], msg[:1024 * mlen].reshape(-1), mlen)
+    sv.verify_fixed(pk[:1024], sig[:1024], msg.reshape(-1)[:1024 * mlen], mlen)
     best = 1e9
     for _ in range(reps):
         t0 = time.perf_counter()
