@@ -153,7 +153,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20, help="signatures per GPU per step")
     ap.add_argument("--latency-iters", type=int, default=200)
-    ap.add_argument("--cpu-sample", type=int, default=262144)
+    ap.add_argument("--cpu-sample", type=int, default=524288)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     args = ap.parse_args()
@@ -265,7 +265,8 @@ def main():
             try:
                 with open(tf) as f:
                     tj = json.load(f)
-                if int(tj.get("batch", -1)) == n:
+                # only when measured on this very kernel source and batch size
+                if int(tj.get("batch", -1)) == n and tj.get("kernel_source_sha256") == sv.kernel_source_digest():
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None

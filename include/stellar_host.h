@@ -73,6 +73,14 @@ void svh_cache_counts(uint64_t* hits, uint64_t* misses); /* flushes, like flushV
 void svh_engine_counts(uint64_t* signatures, uint64_t* batches);
 /* test hook: route cache misses to fn instead of the GPU (NULL restores) */
 void svh_set_test_verifier(svh_batch_verify_fn fn);
+/* Keyed batches: verifySigBatch calls with >= min_items
+ * eligible signatures get verdicts AND BLAKE2b cache keys from one engine pass
+ * (sv_ed25519_verify_batch_keyed); 0 disables; default 4096.  The keyed test
+ * hook replaces that engine call (CPU tests). */
+typedef int (*svh_keyed_verify_fn)(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                                   const uint32_t* len, size_t n, uint8_t* verdict, uint8_t* keys);
+void svh_set_test_keyed_verifier(svh_keyed_verify_fn fn);
+void svh_set_keyed_threshold(size_t min_items);
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs);
 

@@ -112,6 +112,36 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
 int sv_ed25519_sign_device(int device, const void* d_seed, const void* d_msg32, size_t n, void* d_pk,
                            void* d_sig, void* stream);
 
+/* ---- Batch hashing on the device ----------------------
+ * Verify-cache keys: keys[32*i..] = BLAKE2b-256(pk_i || sig_i || msg_i), the key
+ * PubKeyUtils::verifySig computes per call before consulting the cache
+ * (/root/reference/src/crypto/SecretKey.cpp:50-61, verifySigCacheKey).
+ * Message layout as in sv_ed25519_verify_batch. */
+int sv_verify_cache_keys(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                         const uint32_t* msg_len, size_t n, uint8_t* keys /* n x 32 */, const sv_opts* opts);
+
+/* Verdicts AND cache keys from one staging of the batch (one H2D, two kernels
+ * on one stream, one sync): the verifySigBatch miss path without any
+ * per-signature host hashing. */
+int sv_ed25519_verify_batch_keyed(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                                  const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* verdict,
+                                  uint8_t* keys /* n x 32 */, const sv_opts* opts);
+
+/* SHA-256 of n byte strings (data + off[i], len[i]): digests[32*i..].  Batch
+ * form of the transaction contents hash, sha256(xdr(networkID, ENVELOPE_TYPE_TX,
+ * tx)) at /root/reference/src/transactions/TransactionFrame.cpp:90-117. */
+int sv_sha256_batch(const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n,
+                    uint8_t* digests /* n x 32 */, const sv_opts* opts);
+
+/* Device-resident forms (stream semantics as sv_ed25519_verify_device; pk, sig
+ * and output buffers 4-byte aligned; fixed_len != 0 means item i's message is
+ * d_msg + i * fixed_len and d_off / d_len are ignored). */
+int sv_verify_cache_keys_device(int device, const void* d_pk, const void* d_sig, const void* d_msg,
+                                const uint64_t* d_msg_off, const uint32_t* d_msg_len, uint32_t fixed_msg_len,
+                                size_t n, void* d_keys, void* stream);
+int sv_sha256_device(int device, const void* d_data, const uint64_t* d_off, const uint32_t* d_len,
+                     uint32_t fixed_len, size_t n, void* d_digests, void* stream);
+
 /* Kernel-time accounting for profiling: when enabled, every verify launch is
  * bracketed by HIP events on the device's internal stream and the elapsed
  * times are accumulated (read back with sv_kernel_time). */

@@ -23,6 +23,19 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libstellar_sigverify.so")
+
+
+def kernel_source_digest() -> str:
+    """SHA-256 over the device sources (csrc/*.h, *.hip): ties profile-derived
+    numbers (profiles/*_traffic.json) to the kernel they were measured on."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(_HERE, "csrc", "*.h")) + glob.glob(os.path.join(_HERE, "csrc", "*.hip"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 HOSTLIB_PATH = os.path.join(_HERE, "libstellar_host.so")
 
 SV_OK = 0
@@ -39,7 +52,8 @@ EXPORTED_SYMBOLS = (
     "sv_init", "sv_shutdown", "sv_device_count", "sv_last_error_string", "sv_version",
     "sv_ed25519_verify_batch", "sv_ed25519_verify_batch_fixed", "sv_ed25519_verify_device",
     "sv_ed25519_sign_device", "sv_timing_enable", "sv_kernel_time", "sv_kernel_time_reset",
-    "sv_device_synchronize",
+    "sv_device_synchronize", "sv_verify_cache_keys", "sv_ed25519_verify_batch_keyed", "sv_sha256_batch",
+    "sv_verify_cache_keys_device", "sv_sha256_device",
 )
 
 
@@ -90,6 +104,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sv_kernel_time.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     lib.sv_device_synchronize.argtypes = [ctypes.c_int]
+    lib.sv_verify_cache_keys.argtypes = [vp, vp, vp, vp, vp, sz, vp, vp]
+    lib.sv_ed25519_verify_batch_keyed.argtypes = [vp, vp, vp, vp, vp, sz, vp, vp, vp]
+    lib.sv_sha256_batch.argtypes = [vp, vp, vp, sz, vp, vp]
+    lib.sv_verify_cache_keys_device.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_uint32, sz, vp, vp]
+    lib.sv_sha256_device.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, sz, vp, vp]
     _lib = lib
     return lib
 
@@ -149,6 +168,56 @@ def verify_batch(pk, sig, msg, msg_off, msg_len, device: int = -1, max_devices: 
     out = np.zeros(n, np.uint8)
     _check(lib.sv_ed25519_verify_batch(_ptr(pk), _ptr(sig), _ptr(msg), _ptr(off), _ptr(ln), n, _ptr(out),
                                        _opts(device, max_devices)))
+    return out
+
+
+def _var_msgs(msg, msg_off, msg_len, n):
+    msg = np.ascontiguousarray(np.asarray(msg, dtype=np.uint8).reshape(-1))
+    if msg.size == 0:
+        msg = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(np.asarray(msg_off, dtype=np.uint64))
+    ln = np.ascontiguousarray(np.asarray(msg_len, dtype=np.uint32))
+    if off.shape[0] != n or ln.shape[0] != n:
+        raise ValueError("msg_off/msg_len length mismatch")
+    if n and int((off + ln).max()) > msg.size:
+        raise ValueError("message range out of bounds")
+    return msg, off, ln
+
+
+def cache_keys(pk, sig, msg, msg_off, msg_len, device: int = -1, max_devices: int = 0) -> np.ndarray:
+    """n x 32 verify-cache keys BLAKE2b-256(pk || sig || msg) computed on the GPU
+    (SecretKey.cpp:50-61), SURVEY §8 f4."""
+    lib = load_library()
+    pk, sig = _u8(pk, 32), _u8(sig, 64)
+    n = pk.shape[0]
+    msg, off, ln = _var_msgs(msg, msg_off, msg_len, n)
+    keys = np.zeros((n, 32), np.uint8)
+    _check(lib.sv_verify_cache_keys(_ptr(pk), _ptr(sig), _ptr(msg), _ptr(off), _ptr(ln), n, _ptr(keys),
+                                    _opts(device, max_devices)))
+    return keys
+
+
+def verify_batch_keyed(pk, sig, msg, msg_off, msg_len, device: int = -1, max_devices: int = 0):
+    """(verdicts, cache keys) from one staging of the batch."""
+    lib = load_library()
+    pk, sig = _u8(pk, 32), _u8(sig, 64)
+    n = pk.shape[0]
+    msg, off, ln = _var_msgs(msg, msg_off, msg_len, n)
+    out = np.zeros(n, np.uint8)
+    keys = np.zeros((n, 32), np.uint8)
+    _check(lib.sv_ed25519_verify_batch_keyed(_ptr(pk), _ptr(sig), _ptr(msg), _ptr(off), _ptr(ln), n, _ptr(out),
+                                             _ptr(keys), _opts(device, max_devices)))
+    return out, keys
+
+
+def sha256_batch(data, off, length, device: int = -1, max_devices: int = 0) -> np.ndarray:
+    """n x 32 SHA-256 digests of data[off[i]:off[i]+length[i]] on the GPU
+    (batch tx contents hashes, TransactionFrame.cpp:90-117), SURVEY §8 f4."""
+    lib = load_library()
+    n = len(off)
+    data, o, ln = _var_msgs(data, off, length, n)
+    out = np.zeros((n, 32), np.uint8)
+    _check(lib.sv_sha256_batch(_ptr(data), _ptr(o), _ptr(ln), n, _ptr(out), _opts(device, max_devices)))
     return out
 
 

@@ -85,6 +85,17 @@ using BatchVerifyFn = int (*)(const uint8_t* pk, const uint8_t* sig, const uint8
                               const uint32_t* len, size_t n, uint8_t* verdict);
 void setBatchVerifierForTesting(BatchVerifyFn fn);
 
+// Keyed batches: a verifySigBatch call with at least
+// `minItems` eligible signatures sends ALL of them to the engine in one pass
+// that returns verdicts AND the BLAKE2b cache keys (sv_ed25519_verify_batch_keyed),
+// so the host never hashes; cache bookkeeping (hits, in-batch duplicates,
+// misses, insertions, counters) is then identical to the hashed path.
+// 0 disables.  Default 4096.
+void setKeyedBatchThreshold(size_t minItems);
+using KeyedBatchVerifyFn = int (*)(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                                   const uint32_t* len, size_t n, uint8_t* verdict, uint8_t* keys);
+void setKeyedBatchVerifierForTesting(KeyedBatchVerifyFn fn);
+
 // Number of signatures sent to the engine and number of engine calls
 // (batches) since the last flush -- observability for batch sizes.
 void flushEngineCounts(uint64_t& signatures, uint64_t& batches);

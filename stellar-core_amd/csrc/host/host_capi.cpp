@@ -88,6 +88,8 @@ void svh_engine_counts(uint64_t* sigs, uint64_t* batches) {
   if (batches) *batches = b;
 }
 void svh_set_test_verifier(svh_batch_verify_fn fn) { PubKeyUtils::setBatchVerifierForTesting(fn); }
+void svh_set_test_keyed_verifier(svh_keyed_verify_fn fn) { PubKeyUtils::setKeyedBatchVerifierForTesting(fn); }
+void svh_set_keyed_threshold(size_t min_items) { PubKeyUtils::setKeyedBatchThreshold(min_items); }
 
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs) {

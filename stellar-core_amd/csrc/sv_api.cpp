@@ -36,6 +36,9 @@ hipError_t sv_launch_verify(int mode, unsigned grid, const void* pk, const void*
                             void* verdict, void* bitmap, void* ws, const void* btab, hipStream_t s);
 hipError_t sv_launch_sign(unsigned grid, const void* seed, const void* msg, uint64_t n, void* pk, void* sig,
                           void* ws, const void* btab, hipStream_t s);
+hipError_t sv_launch_hash(int kind, unsigned max_blocks, const void* pk, const void* sig, const void* msg,
+                          const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n, void* out,
+                          hipStream_t s);
 }
 
 namespace {
@@ -89,7 +92,7 @@ struct Device {
   void* ws = nullptr;
   hipEvent_t dep_in = nullptr, dep_out = nullptr;
   std::mutex mu;
-  DevBuf pk, sig, msg, off, len, verdict;
+  DevBuf pk, sig, msg, off, len, verdict, keys;
   // timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   std::vector<uint64_t> pending_n;
@@ -188,15 +191,18 @@ int harvest_timing_locked(Device& D) {
   return SV_OK;
 }
 
-// Host-buffer slice on one device: stage, launch, copy verdicts back, sync.
-int verify_host_slice(Device& D, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
-                      const uint64_t* msg_off, const uint32_t* msg_len, uint32_t fixed_len, size_t n,
-                      uint8_t* verdict) {
+// Host-buffer slice on one device: stage once, then launch the verify kernel
+// (verdict != null) and/or the cache-key kernel (keys != null) on the same
+// stream, copy results back, sync.
+int host_slice(Device& D, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+               const uint32_t* msg_len, uint32_t fixed_len, size_t n, uint8_t* verdict, uint8_t* keys) {
   std::lock_guard<std::mutex> g(D.mu);
   SV_HIP(hipSetDevice(D.id));
   int rc;
   if ((rc = ready_locked(D))) return rc;
-  if ((rc = D.pk.ensure(n * 32)) || (rc = D.sig.ensure(n * 64)) || (rc = D.verdict.ensure(n))) return rc;
+  if ((rc = D.pk.ensure(n * 32)) || (rc = D.sig.ensure(n * 64))) return rc;
+  if (verdict && (rc = D.verdict.ensure(n))) return rc;
+  if (keys && (rc = D.keys.ensure(n * 32))) return rc;
   SV_HIP(hipMemcpyAsync(D.pk.p, pk, n * 32, hipMemcpyHostToDevice, D.stream));
   SV_HIP(hipMemcpyAsync(D.sig.p, sig, n * 64, hipMemcpyHostToDevice, D.stream));
   int mode;
@@ -225,11 +231,54 @@ int verify_host_slice(Device& D, const uint8_t* pk, const uint8_t* sig, const ui
     SV_HIP(hipMemcpyAsync(D.len.p, msg_len, n * 4, hipMemcpyHostToDevice, D.stream));
     mode = 1;
   }
-  if ((rc = launch_locked(D, mode, D.pk.p, D.sig.p, D.msg.p, (const uint64_t*)D.off.p, (const uint32_t*)D.len.p,
-                          fixed_len, n, D.verdict.p, nullptr)))
-    return rc;
-  SV_HIP(hipMemcpyAsync(verdict, D.verdict.p, n, hipMemcpyDeviceToHost, D.stream));
+  if (keys) {
+    SV_HIP(sv_launch_hash(0, D.grid * 2, D.pk.p, D.sig.p, D.msg.p, (const uint64_t*)D.off.p,
+                          (const uint32_t*)D.len.p, fixed_len, n, D.keys.p, D.stream));
+    SV_HIP(hipMemcpyAsync(keys, D.keys.p, n * 32, hipMemcpyDeviceToHost, D.stream));
+  }
+  if (verdict) {
+    if ((rc = launch_locked(D, mode, D.pk.p, D.sig.p, D.msg.p, (const uint64_t*)D.off.p,
+                            (const uint32_t*)D.len.p, fixed_len, n, D.verdict.p, nullptr)))
+      return rc;
+    SV_HIP(hipMemcpyAsync(verdict, D.verdict.p, n, hipMemcpyDeviceToHost, D.stream));
+  }
   SV_HIP(hipStreamSynchronize(D.stream));  // packed/offs must outlive the copies
+  return SV_OK;
+}
+
+// SHA-256 of a host slice of byte strings on one device.
+int sha_slice(Device& D, const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t fixed_len,
+              size_t n, uint8_t* out) {
+  std::lock_guard<std::mutex> g(D.mu);
+  SV_HIP(hipSetDevice(D.id));
+  int rc;
+  if ((rc = ready_locked(D))) return rc;
+  if ((rc = D.keys.ensure(n * 32))) return rc;
+  std::vector<uint64_t> offs;
+  std::vector<uint8_t> packed;
+  if (fixed_len != 0) {
+    if ((rc = D.msg.ensure((size_t)n * fixed_len))) return rc;
+    SV_HIP(hipMemcpyAsync(D.msg.p, data, n * (size_t)fixed_len, hipMemcpyHostToDevice, D.stream));
+  } else {
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) total += len[i];
+    packed.resize(std::max<size_t>(total, 1));
+    offs.resize(n);
+    size_t pos = 0;
+    for (size_t i = 0; i < n; ++i) {
+      offs[i] = pos;
+      if (len[i]) memcpy(packed.data() + pos, data + off[i], len[i]);
+      pos += len[i];
+    }
+    if ((rc = D.msg.ensure(packed.size())) || (rc = D.off.ensure(n * 8)) || (rc = D.len.ensure(n * 4))) return rc;
+    SV_HIP(hipMemcpyAsync(D.msg.p, packed.data(), packed.size(), hipMemcpyHostToDevice, D.stream));
+    SV_HIP(hipMemcpyAsync(D.off.p, offs.data(), n * 8, hipMemcpyHostToDevice, D.stream));
+    SV_HIP(hipMemcpyAsync(D.len.p, len, n * 4, hipMemcpyHostToDevice, D.stream));
+  }
+  SV_HIP(sv_launch_hash(1, D.grid * 2, nullptr, nullptr, D.msg.p, (const uint64_t*)D.off.p,
+                        (const uint32_t*)D.len.p, fixed_len, n, D.keys.p, D.stream));
+  SV_HIP(hipMemcpyAsync(out, D.keys.p, n * 32, hipMemcpyDeviceToHost, D.stream));
+  SV_HIP(hipStreamSynchronize(D.stream));
   return SV_OK;
 }
 
@@ -253,10 +302,30 @@ int select_devices(const sv_opts* opts, std::vector<Device*>& out) {
   return SV_OK;
 }
 
-int verify_host(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
-                const uint32_t* msg_len, uint32_t fixed_len, size_t n, uint8_t* verdict, const sv_opts* opts) {
-  if (n == 0) return SV_OK;
-  if (!pk || !sig || !verdict) return fail(SV_ERR_INVALID_ARG, "null buffer");
+// Runs fn(device, lo, hi) for contiguous slices [g*n/G, (g+1)*n/G), one host
+// thread per device; the first failing device's error is reported.
+template <class F>
+int shard(const std::vector<Device*>& devs, size_t n, F fn) {
+  const size_t G = devs.size();
+  if (G == 1) return fn(*devs[0], (size_t)0, n);
+  std::vector<int> rcs(G, SV_OK);
+  std::vector<std::string> errs(G);
+  std::vector<std::thread> th;
+  for (size_t g = 0; g < G; ++g) {
+    const size_t lo = g * n / G, hi = (g + 1) * n / G;
+    if (hi == lo) continue;
+    th.emplace_back([&, g, lo, hi] {
+      rcs[g] = fn(*devs[g], lo, hi);
+      if (rcs[g]) errs[g] = t_err;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (size_t g = 0; g < G; ++g)
+    if (rcs[g]) return fail(rcs[g], "device " + std::to_string(devs[g]->id) + ": " + errs[g]);
+  return SV_OK;
+}
+
+int check_msgs(const uint8_t* msg, const uint64_t* msg_off, const uint32_t* msg_len, uint32_t fixed_len, size_t n) {
   if (fixed_len == 0 && (!msg_off || !msg_len)) return fail(SV_ERR_INVALID_ARG, "null msg_off/msg_len");
   if (!msg) {
     bool any = false;
@@ -265,30 +334,24 @@ int verify_host(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
       for (size_t i = 0; i < n && !any; ++i) any = msg_len[i] != 0;
     if (any) return fail(SV_ERR_INVALID_ARG, "null msg");
   }
-  int rc = ensure_init();
+  return SV_OK;
+}
+
+int verify_host(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                const uint32_t* msg_len, uint32_t fixed_len, size_t n, uint8_t* verdict, uint8_t* keys,
+                const sv_opts* opts) {
+  if (n == 0) return SV_OK;
+  if (!pk || !sig || (!verdict && !keys)) return fail(SV_ERR_INVALID_ARG, "null buffer");
+  int rc = check_msgs(msg, msg_off, msg_len, fixed_len, n);
   if (rc) return rc;
+  if ((rc = ensure_init())) return rc;
   std::vector<Device*> devs;
   if ((rc = select_devices(opts, devs))) return rc;
-  const size_t G = devs.size();
-  if (G == 1) return verify_host_slice(*devs[0], pk, sig, msg, msg_off, msg_len, fixed_len, n, verdict);
-  std::vector<int> rcs(G, SV_OK);
-  std::vector<std::string> errs(G);
-  std::vector<std::thread> th;
-  for (size_t g = 0; g < G; ++g) {
-    const size_t lo = g * n / G, hi = (g + 1) * n / G;
-    if (hi == lo) continue;
-    th.emplace_back([&, g, lo, hi] {
-      rcs[g] = verify_host_slice(*devs[g], pk + 32 * lo, sig + 64 * lo,
-                                 fixed_len ? msg + lo * (size_t)fixed_len : msg,
-                                 fixed_len ? nullptr : msg_off + lo, fixed_len ? nullptr : msg_len + lo,
-                                 fixed_len, hi - lo, verdict + lo);
-      if (rcs[g]) errs[g] = t_err;
-    });
-  }
-  for (auto& t : th) t.join();
-  for (size_t g = 0; g < G; ++g)
-    if (rcs[g]) return fail(rcs[g], "device " + std::to_string(devs[g]->id) + ": " + errs[g]);
-  return SV_OK;
+  return shard(devs, n, [&](Device& D, size_t lo, size_t hi) {
+    return host_slice(D, pk + 32 * lo, sig + 64 * lo, fixed_len ? msg + lo * (size_t)fixed_len : msg,
+                      fixed_len ? nullptr : msg_off + lo, fixed_len ? nullptr : msg_len + lo, fixed_len, hi - lo,
+                      verdict ? verdict + lo : nullptr, keys ? keys + 32 * lo : nullptr);
+  });
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -311,7 +374,7 @@ void sv_shutdown(void) {
       (void)hipEventDestroy(pr.second);
     }
     D->pk.release(); D->sig.release(); D->msg.release();
-    D->off.release(); D->len.release(); D->verdict.release();
+    D->off.release(); D->len.release(); D->verdict.release(); D->keys.release();
     if (D->ws) (void)hipFree(D->ws);
     if (D->btab) (void)hipFree(D->btab);
     if (D->dep_in) (void)hipEventDestroy(D->dep_in);
@@ -337,7 +400,7 @@ const char* sv_version(void) {
 
 int sv_ed25519_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                             const uint32_t* msg_len, size_t n, uint8_t* verdict, const sv_opts* opts) {
-  return verify_host(pk, sig, msg, msg_off, msg_len, 0, n, verdict, opts);
+  return verify_host(pk, sig, msg, msg_off, msg_len, 0, n, verdict, nullptr, opts);
 }
 
 int sv_ed25519_verify_batch_fixed(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_len,
@@ -347,9 +410,72 @@ int sv_ed25519_verify_batch_fixed(const uint8_t* pk, const uint8_t* sig, const u
     std::vector<uint64_t> off(n, 0);
     std::vector<uint32_t> len(n, 0);
     static const uint8_t dummy = 0;
-    return verify_host(pk, sig, &dummy, off.data(), len.data(), 0, n, verdict, opts);
+    return verify_host(pk, sig, &dummy, off.data(), len.data(), 0, n, verdict, nullptr, opts);
   }
-  return verify_host(pk, sig, msg, nullptr, nullptr, msg_len, n, verdict, opts);
+  return verify_host(pk, sig, msg, nullptr, nullptr, msg_len, n, verdict, nullptr, opts);
+}
+
+int sv_ed25519_verify_batch_keyed(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                                  const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* verdict,
+                                  uint8_t* keys, const sv_opts* opts) {
+  if (!verdict || !keys) return n ? fail(SV_ERR_INVALID_ARG, "null verdict/keys") : SV_OK;
+  return verify_host(pk, sig, msg, msg_off, msg_len, 0, n, verdict, keys, opts);
+}
+
+int sv_verify_cache_keys(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                         const uint32_t* msg_len, size_t n, uint8_t* keys, const sv_opts* opts) {
+  if (!keys) return n ? fail(SV_ERR_INVALID_ARG, "null keys") : SV_OK;
+  return verify_host(pk, sig, msg, msg_off, msg_len, 0, n, nullptr, keys, opts);
+}
+
+int sv_sha256_batch(const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n, uint8_t* digests,
+                    const sv_opts* opts) {
+  if (n == 0) return SV_OK;
+  if (!digests) return fail(SV_ERR_INVALID_ARG, "null digests");
+  int rc = check_msgs(data, off, len, 0, n);
+  if (rc) return rc;
+  if ((rc = ensure_init())) return rc;
+  std::vector<Device*> devs;
+  if ((rc = select_devices(opts, devs))) return rc;
+  return shard(devs, n, [&](Device& D, size_t lo, size_t hi) {
+    return sha_slice(D, data, off + lo, len + lo, 0, hi - lo, digests + 32 * lo);
+  });
+}
+
+// Device-resident hashing (caller's stream ordering as in sv_ed25519_verify_device).
+static int hash_device(int kind, int device, const void* d_pk, const void* d_sig, const void* d_msg,
+                       const uint64_t* d_off, const uint32_t* d_len, uint32_t fixed_len, size_t n, void* d_out,
+                       void* stream) {
+  int rc = ensure_init();
+  if (rc) return rc;
+  if (device < 0 || device >= (int)g_devs.size()) return fail(SV_ERR_INVALID_ARG, "device index out of range");
+  if (n == 0) return SV_OK;
+  if (!d_out || !d_msg || (kind == 0 && (!d_pk || !d_sig))) return fail(SV_ERR_INVALID_ARG, "null device buffer");
+  if (fixed_len == 0 && (!d_off || !d_len)) return fail(SV_ERR_INVALID_ARG, "null msg_off/msg_len");
+  if ((((uintptr_t)d_out) & 3u) || (kind == 0 && ((((uintptr_t)d_pk) & 3u) || (((uintptr_t)d_sig) & 3u))))
+    return fail(SV_ERR_ALIGN, "pk/sig/out must be 4-byte aligned");
+  Device& D = *g_devs[device];
+  std::lock_guard<std::mutex> g(D.mu);
+  SV_HIP(hipSetDevice(D.id));
+  if ((rc = ready_locked(D))) return rc;
+  hipStream_t user = (hipStream_t)stream;
+  SV_HIP(hipEventRecord(D.dep_in, user));
+  SV_HIP(hipStreamWaitEvent(D.stream, D.dep_in, 0));
+  SV_HIP(sv_launch_hash(kind, D.grid * 2, d_pk, d_sig, d_msg, d_off, d_len, fixed_len, n, d_out, D.stream));
+  SV_HIP(hipEventRecord(D.dep_out, D.stream));
+  SV_HIP(hipStreamWaitEvent(user, D.dep_out, 0));
+  return SV_OK;
+}
+
+int sv_verify_cache_keys_device(int device, const void* d_pk, const void* d_sig, const void* d_msg,
+                                const uint64_t* d_msg_off, const uint32_t* d_msg_len, uint32_t fixed_msg_len,
+                                size_t n, void* d_keys, void* stream) {
+  return hash_device(0, device, d_pk, d_sig, d_msg, d_msg_off, d_msg_len, fixed_msg_len, n, d_keys, stream);
+}
+
+int sv_sha256_device(int device, const void* d_data, const uint64_t* d_off, const uint32_t* d_len,
+                     uint32_t fixed_len, size_t n, void* d_digests, void* stream) {
+  return hash_device(1, device, nullptr, nullptr, d_data, d_off, d_len, fixed_len, n, d_digests, stream);
 }
 
 int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, const void* d_msg,

@@ -50,7 +50,7 @@ def test_host_library_exports_every_declared_symbol(sv):
     if not os.path.exists(sv.HOSTLIB_PATH):
         subprocess.run(["make", "-s", "-j4"], cwd=os.path.join(REPO, "stellar-core_amd"), check=True)
     src = re.sub(r"/\*.*?\*/", "", open(os.path.join(REPO, "include", "stellar_host.h")).read(), flags=re.S)
-    names = sorted(set(re.findall(r"\b(svh_[a-z0-9_]+)\s*\(", src)) - {"svh_batch_verify_fn"})
+    names = sorted(set(re.findall(r"\b(svh_[a-z0-9_]+)\s*\(", src)) - {"svh_batch_verify_fn", "svh_keyed_verify_fn"})
     assert "svh_mb_run" in names and "svh_check_txset" in names
     lib = ctypes.CDLL(sv.HOSTLIB_PATH)
     for name in names:
@@ -76,6 +76,12 @@ def test_no_cpu_fallback_without_gpu(sv):
         sv.verify_batch(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"])
     with pytest.raises(sv.SigVerifyError):
         sv.verify_fixed(d["pk"][:2], d["sig"][:2], np.zeros(64, np.uint8))
+    with pytest.raises(sv.SigVerifyError):
+        sv.verify_batch_keyed(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"])
+    with pytest.raises(sv.SigVerifyError):
+        sv.cache_keys(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"])
+    with pytest.raises(sv.SigVerifyError):
+        sv.sha256_batch(d["msg"], d["msg_off"], d["msg_len"])
 
 
 def test_python_binding_validates_shapes(sv):

@@ -222,3 +222,35 @@ def test_oracle_crosscheck_random_adversarial_gpu(sv, dev, oracle):
          "msg_len": np.full(n, 32, np.uint32), "verdict": out}
     want = oracle_verdicts(oracle, d)
     assert np.array_equal(out, want)
+
+
+@pytest.mark.gpu
+def test_gpu_cache_keys_and_keyed_verify(sv, golden):
+    """f4: BLAKE2b-256(pk||sig||msg) cache keys on the GPU == hashlib; the keyed
+    verify returns the same verdicts as the plain one (libsodium's)."""
+    for name in ("intree", "msglen", "adversarial"):
+        d = golden[name]
+        keys = sv.cache_keys(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"])
+        v2, k2 = sv.verify_batch_keyed(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"])
+        assert (v2 == d["verdict"]).all(), name
+        assert (k2 == keys).all(), name
+        for i in range(0, len(keys), max(1, len(keys) // 300)):
+            o, ln = int(d["msg_off"][i]), int(d["msg_len"][i])
+            want = hashlib.blake2b(d["pk"][i].tobytes() + d["sig"][i].tobytes() + d["msg"][o:o + ln].tobytes(),
+                                   digest_size=32).digest()
+            assert keys[i].tobytes() == want, (name, i)
+
+
+@pytest.mark.gpu
+def test_gpu_sha256_batch(sv):
+    """f4: batch SHA-256 on the GPU == hashlib for every length 0..300 and
+    4 KiB tx-sized bodies at arbitrary (unaligned) offsets."""
+    rng = np.random.default_rng(21)
+    lens = np.array(list(range(0, 301)) + [4096, 4097, 65535], np.uint32)
+    off = np.zeros(len(lens), np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + 3)  # odd gaps: misaligned starts
+    data = rng.integers(0, 256, int(off[-1] + lens[-1]), dtype=np.uint8)
+    got = sv.sha256_batch(data, off, lens)
+    for i in range(len(lens)):
+        o, ln = int(off[i]), int(lens[i])
+        assert got[i].tobytes() == hashlib.sha256(data[o:o + ln].tobytes()).digest(), ln

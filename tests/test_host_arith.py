@@ -178,3 +178,38 @@ def test_lane_verifier_matches_golden(hostcore, golden):
         got = _host_verify(hostcore, d, rows)
         bad = np.nonzero(got != d["verdict"][rows])[0]
         assert len(bad) == 0, (name, [str(d["class_names"][d["cls"][rows[i]]]) for i in bad[:10]])
+
+
+def _hash_inputs(rnd, n):
+    """Bytes at a random misalignment inside a larger buffer (the device code
+    reads aligned dwords around them)."""
+    pad = rnd.integers(0, 4)
+    buf = bytes(rnd.integers(0, 256, int(pad) + n + 8, dtype=np.uint8))
+    return buf, int(pad)
+
+
+def test_device_blake2b_cache_key(hostcore):
+    """hash_dev.h sv_cache_key == BLAKE2b-256(pk || sig || msg) (RFC 7693,
+    hashlib), the verify-cache key of SecretKey.cpp:50-61."""
+    rnd = np.random.default_rng(11)
+    out = ctypes.create_string_buffer(32)
+    for n in list(range(0, 70)) + [127, 128, 129, 159, 160, 161, 255, 256, 257, 300, 1000]:
+        pk, sig = rnd.bytes(32), rnd.bytes(64)
+        buf, pad = _hash_inputs(rnd, n)
+        base = ctypes.create_string_buffer(buf, len(buf))
+        hostcore.hc_cache_key(out, pk, sig, ctypes.byref(base, pad), ctypes.c_uint32(n))
+        assert out.raw == hashlib.blake2b(pk + sig + buf[pad:pad + n], digest_size=32).digest(), n
+
+
+def test_device_sha256(hostcore):
+    """hash_dev.h sv_sha256 == SHA-256 (FIPS 180-4, hashlib) at every padding
+    boundary; the tx contents hash of TransactionFrame.cpp:90-117."""
+    rnd = np.random.default_rng(12)
+    out = ctypes.create_string_buffer(32)
+    for n in list(range(0, 140)) + [183, 184, 191, 192, 247, 248, 1000, 4097]:
+        buf, pad = _hash_inputs(rnd, n)
+        base = ctypes.create_string_buffer(buf, len(buf))
+        hostcore.hc_sha256(out, ctypes.byref(base, pad), ctypes.c_uint32(n))
+        assert out.raw == hashlib.sha256(buf[pad:pad + n]).digest(), n
+    hostcore.hc_sha256(out, b"abc", 3)  # FIPS 180-2 appendix B.1
+    assert out.raw.hex() == "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"

@@ -32,6 +32,8 @@ def host(sv):
                                    ctypes.c_size_t]
     lib.svh_last_error_string.restype = ctypes.c_char_p
     lib.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+    lib.svh_set_test_keyed_verifier.argtypes = [ctypes.c_void_p]
+    lib.svh_set_keyed_threshold.argtypes = [ctypes.c_size_t]
     return lib
 
 
@@ -57,7 +59,33 @@ class OracleEngine:
                                                            pkb[32 * i:32 * i + 32]) == 0 else 0
             return 0
 
+        self.fn_plain = fn
         self.cfn = VERIFY_FN(fn)
+
+
+KEYED_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p)
+
+
+class OracleKeyedEngine(OracleEngine):
+    """Keyed engine stand-in (f4): oracle verdicts + hashlib BLAKE2b-256 keys."""
+
+    def __init__(self, oracle):
+        super().__init__(oracle)
+
+        def kfn(pk, sig, msg, off, ln, n, out, keys):
+            self.fn_plain(pk, sig, msg, off, ln, n, out)
+            offs = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (n,))
+            lens = np.ctypeslib.as_array(ctypes.cast(ln, ctypes.POINTER(ctypes.c_uint32)), (n,))
+            kb = np.ctypeslib.as_array(ctypes.cast(keys, ctypes.POINTER(ctypes.c_uint8)), (n * 32,))
+            for i in range(n):
+                m = ctypes.string_at(msg + int(offs[i]), int(lens[i])) if lens[i] else b""
+                d = hashlib.blake2b(ctypes.string_at(pk + 32 * i, 32) + ctypes.string_at(sig + 64 * i, 64) + m,
+                                    digest_size=32).digest()
+                kb[32 * i:32 * i + 32] = np.frombuffer(d, np.uint8)
+            return 0
+
+        self.kcfn = KEYED_FN(kfn)
 
 
 @pytest.fixture()
@@ -130,6 +158,50 @@ def test_verify_sig_batch_dedup_and_verdicts(host, engine, golden):
     assert (out == d["verdict"][rows]).all()
     assert engine.calls == 1 and engine.sigs == n - 20
     assert _counts(host) == (20, n - 20)
+
+
+def test_verify_sig_batch_keyed_path(host, oracle, golden):
+    """f4: with the keyed pass (verdicts + cache keys from the engine, no host
+    hashing) verdicts, hit/miss counters and cache contents match the hashed
+    path exactly; the engine sees every eligible row in ONE call."""
+    e = OracleKeyedEngine(oracle)
+    host.svh_set_test_verifier(None)
+    host.svh_set_test_keyed_verifier(ctypes.cast(e.kcfn, ctypes.c_void_p))
+    host.svh_set_keyed_threshold(1)
+    host.svh_cache_clear()
+    host.svh_cache_counts(None, None)
+    try:
+        d = golden["adversarial"]
+        rows = np.arange(0, len(d["verdict"]), 13)
+        rows = np.concatenate([rows, rows[:15]])
+        n = len(rows)
+        pk = np.ascontiguousarray(d["pk"][rows])
+        sig = np.ascontiguousarray(d["sig"][rows])
+        off = np.ascontiguousarray(d["msg_off"][rows])
+        ln = np.ascontiguousarray(d["msg_len"][rows])
+        msg = np.ascontiguousarray(d["msg"])
+        for rep in range(2):
+            out = np.zeros(n, np.uint8)
+            rc = host.svh_verify_sig_batch(pk.ctypes.data_as(ctypes.c_void_p), sig.ctypes.data_as(ctypes.c_void_p),
+                                           None, msg.ctypes.data_as(ctypes.c_void_p),
+                                           off.ctypes.data_as(ctypes.c_void_p), ln.ctypes.data_as(ctypes.c_void_p),
+                                           ctypes.c_size_t(n), out.ctypes.data_as(ctypes.c_void_p))
+            assert rc == 0, host.svh_last_error_string()
+            assert (out == d["verdict"][rows]).all()
+            if rep == 0:
+                assert _counts(host) == (15, n - 15)  # in-batch duplicates count as hits
+            else:
+                assert _counts(host) == (n, 0)        # every key now cached
+        assert e.sigs == 2 * n and e.calls == 2       # one keyed engine pass per batch
+        # a single verifySig now hits the entry the keyed batch stored
+        i = 0
+        o, L = int(off[i]), int(ln[i])
+        assert host.svh_verify_sig(pk[i].tobytes(), sig[i].tobytes(), 64, msg[o:o + L].tobytes(), L) == d["verdict"][rows[i]]
+        assert _counts(host) == (1, 0)
+    finally:
+        host.svh_set_test_keyed_verifier(None)
+        host.svh_set_keyed_threshold(4096)
+        host.svh_cache_clear()
 
 
 def _oracle_sign_fn(oracle):
@@ -256,3 +328,41 @@ def test_micro_batcher_deadline_flush(host, engine, golden):
     assert (out == 1).all()
     assert st.flushed_by_size == 0 and st.flushed_by_deadline >= 1
     assert st.lat_p99_us >= 0 and st.items == 5
+
+
+@pytest.mark.gpu
+def test_gpu_verify_sig_batch_keyed_matches_hashed(host, sv, golden):
+    """f4 on the GPU: the keyed pass (engine returns cache keys) gives the same
+    verdicts and hit/miss counts as host BLAKE2b hashing."""
+    if sv.device_count() < 1:
+        pytest.skip("no GPU")
+    host.svh_set_test_verifier(None)
+    host.svh_set_test_keyed_verifier(None)
+    d = golden["adversarial"]
+    rows = np.arange(len(d["verdict"]))
+    rows = np.concatenate([rows, rows[:100]])
+    n = len(rows)
+    pk = np.ascontiguousarray(d["pk"][rows])
+    sig = np.ascontiguousarray(d["sig"][rows])
+    off = np.ascontiguousarray(d["msg_off"][rows])
+    ln = np.ascontiguousarray(d["msg_len"][rows])
+    msg = np.ascontiguousarray(d["msg"])
+    res = []
+    try:
+        for thr in (0, 1):
+            host.svh_set_keyed_threshold(thr)
+            host.svh_cache_clear()
+            host.svh_cache_counts(None, None)
+            out = np.zeros(n, np.uint8)
+            rc = host.svh_verify_sig_batch(pk.ctypes.data_as(ctypes.c_void_p), sig.ctypes.data_as(ctypes.c_void_p),
+                                           None, msg.ctypes.data_as(ctypes.c_void_p),
+                                           off.ctypes.data_as(ctypes.c_void_p), ln.ctypes.data_as(ctypes.c_void_p),
+                                           ctypes.c_size_t(n), out.ctypes.data_as(ctypes.c_void_p))
+            assert rc == 0, host.svh_last_error_string()
+            res.append((out.copy(), _counts(host)))
+    finally:
+        host.svh_set_keyed_threshold(4096)
+        host.svh_cache_clear()
+    assert (res[0][0] == d["verdict"][rows]).all()
+    assert (res[1][0] == res[0][0]).all()
+    assert res[0][1] == res[1][1]

@@ -72,8 +72,16 @@ def main():
         out["valu_active_frac_of_wave_cycles"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
     if "SQ_BUSY_CYCLES" in avg and "SQ_ACTIVE_INST_VALU" in avg:
         out["note"] = "SQ_* cycle counters are in quad-cycles (MI355X_MICROARCH.md)"
+    if "SQ_INSTS_VALU" in avg and "avg_ns" in out:
+        # each wave64 VALU instruction occupies its SIMD for 4 cycles (1024 SIMDs)
+        ghz = out.get("effective_clock_ghz", 2.4)
+        out["valu_issue_util"] = avg["SQ_INSTS_VALU"] * 4 / (1024 * out["avg_ns"] * ghz)
     if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
         out["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import importlib
+    os.environ.setdefault("SV_NO_TORCH", "1")
+    out["kernel_source_sha256"] = importlib.import_module("stellar-core_amd").kernel_source_digest()
     print(json.dumps(out, indent=1))
 
 
