@@ -260,6 +260,7 @@ def main():
     if rank == 0:
         achieved = kernel_rate * W_MAD_PER_VERIFY / 1e12
         traffic = None
+        prof = {}
         tf = os.path.join(REPO, "profiles", "r01_traffic.json")
         if os.path.exists(tf):
             try:
@@ -268,6 +269,9 @@ def main():
                 # only when measured on this very kernel source and batch size
                 if int(tj.get("batch", -1)) == n and tj.get("kernel_source_sha256") == sv.kernel_source_digest():
                     traffic = tj.get("hbm_bytes_per_launch")
+                    prof = {k: tj[k] for k in ("valu_inst_per_verify", "valu_issue_util", "l2_hit_rate",
+                                               "kernel_avg_ns") if k in tj}
+                    prof["source"] = "profiles/r01_traffic.json (rocprofv3 PMC, tools/profile_run.sh)"
             except Exception:
                 traffic = None
         result = {
@@ -306,6 +310,8 @@ def main():
                 "algorithmic_per_verify": W_MAD_PER_VERIFY,
                 "peak_source": PEAK_SOURCE,
                 "frac_vs_survey_nominal_peak": kernel_rate * W_MAD_PER_VERIFY / NOMINAL_PEAK_SURVEY,
+                "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE)",
+                "profiled": prof or None,
             },
         }
 

@@ -25,17 +25,22 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libstellar_sigverify.so")
 
 
+VERIFY_KERNEL_SOURCES = ("sv_common.h", "fe25519.h", "ge25519.h", "sc25519.h", "sha512_dev.h", "verify_core.h",
+                         "sv_kernels.hip")
+
+
 def kernel_source_digest() -> str:
-    """SHA-256 over the device sources (csrc/*.h, *.hip): ties profile-derived
+    """SHA-256 over the verify kernel's device sources: ties profile-derived
     numbers (profiles/*_traffic.json) to the kernel they were measured on."""
-    import glob
     import hashlib
     h = hashlib.sha256()
-    for f in sorted(glob.glob(os.path.join(_HERE, "csrc", "*.h")) + glob.glob(os.path.join(_HERE, "csrc", "*.hip"))):
-        h.update(os.path.basename(f).encode())
-        with open(f, "rb") as fh:
+    for name in VERIFY_KERNEL_SOURCES:
+        h.update(name.encode())
+        with open(os.path.join(_HERE, "csrc", name), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()
+
+
 HOSTLIB_PATH = os.path.join(_HERE, "libstellar_host.so")
 
 SV_OK = 0
