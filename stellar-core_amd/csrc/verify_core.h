@@ -17,9 +17,9 @@
 //   d_A in [-8, 8] (signed radix 16 of h); on every 4th window also add
 //   table_B[d_B], d_B in [-2^15, 2^15] (signed radix 2^16 of S; SV_B_BITS).
 //   table_A = {0..8}·(-A) in cached form, built per lane into an HBM workspace
-//   slot (1728 B/lane, lane-major so a lane's entry is 192 contiguous bytes;
-//   too big for LDS at >= 2 waves/SIMD), each window's entry prefetched into
-//   LDS by DMA while the window doubles;
+//   slot (1584 B/lane, lane-major so a lane's entry is 176 contiguous bytes;
+//   too big for LDS at >= 2 waves/SIMD); each window's table_A and table_B
+//   entries are prefetched into LDS by DMA while the window doubles;
 //   table_B = {0..2^15}·B in affine precomp form, one global copy per device.
 //   Zero digits add the identity entry, so every lane does identical work.
 #pragma once
@@ -46,9 +46,11 @@ struct __attribute__((aligned(16))) sv_u4 {
 #define SV_BTAB_ENTRIES ((1 << (SV_B_BITS - 1)) + 1)
 #define SV_BTAB_STRIDE 36
 #define SV_BTAB_DWORDS (SV_BTAB_ENTRIES * SV_BTAB_STRIDE)
-// A-table (HBM workspace): 9 entries x 12 quads: YpX YmX Z T2d (3 quads each)
+// A-table (HBM workspace): 9 entries x 11 quads: YpX (3 quads) YmX (3 quads)
+// then Z and T2d packed back to back (20 dwords = 5 quads; only the pair that
+// a negative digit swaps needs the 3-quad padding).
 #define SV_ATAB_ENTRIES 9
-#define SV_ATAB_QUADS 12
+#define SV_ATAB_QUADS 11
 // Signatures per lane whose final inversions are batched (Montgomery trick),
 // and the per-lane workspace slot: table_A + K pending points (X, Y, Z).
 #define SV_BATCH_K 4
@@ -92,12 +94,28 @@ SV_HD void sv_load_fe3(fe& f, const sv_u4* p, int qstride) {
   f.v[8] = c.x; f.v[9] = c.y;
 }
 
+// two field elements packed in 5 quads (20 dwords)
+SV_HD void sv_store_fe_pair(sv_u4* p, int qstride, const fe& a, const fe& b) {
+  p[0] = sv_u4{a.v[0], a.v[1], a.v[2], a.v[3]};
+  p[qstride] = sv_u4{a.v[4], a.v[5], a.v[6], a.v[7]};
+  p[2 * qstride] = sv_u4{a.v[8], a.v[9], b.v[0], b.v[1]};
+  p[3 * qstride] = sv_u4{b.v[2], b.v[3], b.v[4], b.v[5]};
+  p[4 * qstride] = sv_u4{b.v[6], b.v[7], b.v[8], b.v[9]};
+}
+SV_HD void sv_load_fe_pair(fe& a, fe& b, const sv_u4* p, int qstride) {
+  const sv_u4 q0 = p[0], q1 = p[qstride], q2 = p[2 * qstride], q3 = p[3 * qstride], q4 = p[4 * qstride];
+  a.v[0] = q0.x; a.v[1] = q0.y; a.v[2] = q0.z; a.v[3] = q0.w;
+  a.v[4] = q1.x; a.v[5] = q1.y; a.v[6] = q1.z; a.v[7] = q1.w;
+  a.v[8] = q2.x; a.v[9] = q2.y; b.v[0] = q2.z; b.v[1] = q2.w;
+  b.v[2] = q3.x; b.v[3] = q3.y; b.v[4] = q3.z; b.v[5] = q3.w;
+  b.v[6] = q4.x; b.v[7] = q4.y; b.v[8] = q4.z; b.v[9] = q4.w;
+}
+
 SV_HD void sv_store_cached(sv_u4* slot, int qstride, int e, const ge_cached& c) {
   sv_u4* base = slot + e * SV_ATAB_QUADS * qstride;
   sv_store_fe3(base, qstride, c.YpX);
   sv_store_fe3(base + 3 * qstride, qstride, c.YmX);
-  sv_store_fe3(base + 6 * qstride, qstride, c.Z);
-  sv_store_fe3(base + 9 * qstride, qstride, c.T2d);
+  sv_store_fe_pair(base + 6 * qstride, qstride, c.Z, c.T2d);
 }
 
 // table_A = {0..8}·(-A) in cached form, written to the lane's workspace slot.
@@ -123,8 +141,14 @@ SV_COLD void sv_build_atab(sv_u4* slot, int qstride, const ge_p3& negA) {
 // Step machine: per window w (64 of them, MSB first) run steps
 //   s = 0..3  doubling, s = 4  add table_A[d_A], s = 5 (even w) add table_B[d_B]
 // with one code instance of each step kind; every branch is wave-uniform.
-// Per-wave LDS stage for the next table_A entry: [12 quads][64 lanes] x 16 B.
-#define SV_STAGE_QUADS (SV_ATAB_QUADS * 64)
+// Per-wave LDS stage: the window's table_A entry [11 quads][64 lanes] x 16 B,
+// then (SV_STAGE_B) its table_B entry [9 quads][64 lanes] -- 20 KiB per wave,
+// so two 256-thread workgroups fill the CU's 160 KiB.
+#ifndef SV_STAGE_B
+#define SV_STAGE_B (SV_B_BITS == 16)  // (an LDS-resident radix-256 table needs no stage)
+#endif
+#define SV_BTAB_QUADS (SV_BTAB_STRIDE / 4)
+#define SV_STAGE_QUADS ((SV_ATAB_QUADS + (SV_STAGE_B ? SV_BTAB_QUADS : 0)) * 64)
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // Device: the window's table_A entry is fetched by LDS-DMA (global_load_lds,
@@ -143,6 +167,18 @@ SV_HD void sv_stage_aentry(sv_u4* stage, const sv_u4* slot, int qstride, int32_t
   SV_UNROLL for (int q = 0; q < SV_ATAB_QUADS; ++q) {
     const sv_u4* src = q < 3 ? ea + q * qstride : (q < 6 ? eb + (q - 3) * qstride : e + q * qstride);
     __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(stage + q * 64),
+                                     16, 0, 0);
+  }
+}
+// Same for the window's table_B entry (4.7 MB global table, L2/MALL-hot).
+SV_HD void sv_stage_bentry(sv_u4* stageB, const sv_u4* btab, int32_t d) {
+  const bool neg = d < 0;
+  const sv_u4* e = btab + (neg ? -d : d) * SV_BTAB_QUADS;
+  const sv_u4* ea = e + (neg ? 3 : 0);
+  const sv_u4* eb = e + (neg ? 0 : 3);
+  SV_UNROLL for (int q = 0; q < SV_BTAB_QUADS; ++q) {
+    const sv_u4* src = q < 3 ? ea + q : (q < 6 ? eb + (q - 3) : e + q);
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(stageB + q * 64),
                                      16, 0, 0);
   }
 }
@@ -173,8 +209,12 @@ SV_HD void sv_double_scalarmult(ge_p3& P, const ge_p3& negA, const uint32_t h[8]
   SV_NOUNROLL for (int w = 63; w >= 0; --w) {
     const int nsteps = (w & (SV_B_BITS / 4 - 1)) ? 5 : 6;
     const int32_t dA = sc_pop_top(da, 4);
+    const int32_t dB = nsteps == 6 ? sc_pop_top(db, SV_B_BITS) : 0;
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (STAGED) sv_stage_aentry(stage, slot, qstride, dA);
+    if (STAGED) {
+      sv_stage_aentry(stage, slot, qstride, dA);
+      if (SV_STAGE_B && nsteps == 6) sv_stage_bentry(stage + SV_ATAB_QUADS * 64, btab, dB);
+    }
 #endif
     SV_NOUNROLL for (int s = 0; s < nsteps; ++s) {
       if (s < 4) {
@@ -194,25 +234,33 @@ SV_HD void sv_double_scalarmult(ge_p3& P, const ge_p3& negA, const uint32_t h[8]
             const sv_u4* st = stage + __lane_id();
             sv_load_fe3(qa, st, 64);
             sv_load_fe3(qb, st + 3 * 64, 64);
-            sv_load_fe3(qz, st + 6 * 64, 64);
-            sv_load_fe3(qt, st + 9 * 64, 64);
+            sv_load_fe_pair(qz, qt, st + 6 * 64, 64);
           } else
 #endif
           {
             const sv_u4* e = slot + (neg ? -dA : dA) * SV_ATAB_QUADS * qstride;
             sv_load_fe3(qa, e + (neg ? 3 : 0) * qstride, qstride);
             sv_load_fe3(qb, e + (neg ? 0 : 3) * qstride, qstride);
-            sv_load_fe3(qz, e + 6 * qstride, qstride);
-            sv_load_fe3(qt, e + 9 * qstride, qstride);
+            sv_load_fe_pair(qz, qt, e + 6 * qstride, qstride);
           }
         } else {
-          const int32_t d = sc_pop_top(db, SV_B_BITS);
-          neg = d < 0;
-          const sv_u4* e = btab + (neg ? -d : d) * (SV_BTAB_STRIDE / 4);
-          sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
-          sv_load_fe3(qb, e + (neg ? 0 : 3), 1);
+          neg = dB < 0;
           fe_1(qz);
-          sv_load_fe3(qt, e + 6, 1);
+#if defined(__HIP_DEVICE_COMPILE__)
+          if (STAGED && SV_STAGE_B) {
+            sv_stage_wait();
+            const sv_u4* st = stage + SV_ATAB_QUADS * 64 + __lane_id();
+            sv_load_fe3(qa, st, 64);
+            sv_load_fe3(qb, st + 3 * 64, 64);
+            sv_load_fe3(qt, st + 6 * 64, 64);
+          } else
+#endif
+          {
+            const sv_u4* e = btab + (neg ? -dB : dB) * SV_BTAB_QUADS;
+            sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
+            sv_load_fe3(qb, e + (neg ? 0 : 3), 1);
+            sv_load_fe3(qt, e + 6, 1);
+          }
         }
         ge_add_preswapped(Q, P, qa, qb, qz, qt, neg, zone);
       }

@@ -20,6 +20,7 @@ for p in paths:
                                    ctypes.POINTER(ctypes.c_uint64)]
     assert lib.sv_init() == 0
     libs[os.path.basename(p)] = lib
+    print("%-28s resident workgroups/CU: %d" % (os.path.basename(p), lib.sv_occupancy_blocks_per_cu()), flush=True)
 
 dev = torch.device("cuda", 0)
 n = 1 << 20
