@@ -25,7 +25,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libstellar_sigverify.so")
 
 
-VERIFY_KERNEL_SOURCES = ("sv_common.h", "fe25519.h", "ge25519.h", "sc25519.h", "sha512_dev.h", "verify_core.h",
+VERIFY_KERNEL_SOURCES = ("sv_common.h", "fe25519.h", "ge25519.h", "sc25519.h", "lattice.h", "sha512_dev.h", "verify_core.h",
                          "sv_kernels.hip")
 
 

@@ -22,6 +22,13 @@
 #define SV_STAGE_A 1  // table_A entries via LDS-DMA prefetch (verify_core.h)
 #endif
 #define SV_WAVES_PER_SIMD 2
+// 1: verify through the half-size equation (lattice.h, ~130 doublings per
+// signature); 0: the direct 253-bit ladder (sv_verify_kernel below).
+#ifndef SV_LATTICE
+#define SV_LATTICE 1
+#endif
+// base-point tables in the device buffer: e·B, then (SV_LATTICE) e·(2^128 B)
+#define SV_NBTAB (SV_LATTICE ? 2 : 1)
 
 struct sv_kparams {
   const sv_u4* pk;        // n x 32 B (2 quads)
@@ -136,9 +143,94 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_kernel(
   }
 }
 
+// Half-size verification (lattice.h): one signature per lane per wave
+// iteration.  Per lane: checks (1)-(5) + decode of R, Euclid reduction of h,
+// tables of -A and -R in the workspace slot; the wave then runs W windows,
+// W = the maximum over its lanes (33 for ~91% of waves, 34 for most others),
+// and each lane accepts iff P' is the identity.  No inversion is needed.
+// SV_PHASE_PROF (developer builds only, tools/phase_prof.py): lane 0 of every
+// wave accumulates s_memtime deltas per phase into sv_phase_cycles.
+#ifdef SV_PHASE_PROF
+__device__ unsigned long long sv_phase_cycles[8];
+#define SV_PHASE(k)                                              \
+  do {                                                           \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
+    if (lane == 0) atomicAdd(&sv_phase_cycles[k], t_ - t_prev);  \
+    t_prev = t_;                                                 \
+  } while (0)
+#else
+#define SV_PHASE(k) ((void)0)
+#endif
+
+template <int MODE>
+__global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_lat_kernel(sv_kparams p) {
+  __shared__ sv_u4 s_stage[SV_BLOCK / 64][2 * SV_LTAB_QUADS * 64];  // per-wave A and R entry stage
+  const uint32_t lane = threadIdx.x & 63u;
+  sv_u4* stage = s_stage[threadIdx.x >> 6];
+  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  sv_u4* tabA = p.ws + gtid * SV_SLOT_QUADS;
+  sv_u4* tabR = tabA + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
+  const sv_u4* btab0 = p.btab;
+  const sv_u4* btab1 = p.btab + SV_BTAB_ENTRIES * SV_BTAB_QUADS;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+
+  for (uint64_t base = gtid - lane; base < p.n; base += stride) {
+    const uint64_t i = base + lane;
+    const bool active = i < p.n;
+    const uint64_t ii = active ? i : p.n - 1;  // idle tail lanes redo the last item
+#ifdef SV_PHASE_PROF
+    unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+#endif
+    uint32_t A[8], S[8], hram[16], R[8];
+    sv_load_and_hash<MODE>(p, ii, A, S, hram);
+    sv_unpack2(R, p.sig + 4 * ii);
+    SV_PHASE(0);
+    sv_lat lat;
+#ifdef SV_PHASE_PROF
+    bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
+              sv_point_canonical(R);
+    ge_p3 negA, negR;
+    ok = ge_frombytes(negA, A, true) && ok;
+    ok = ge_frombytes(negR, R, true) && ok;
+    SV_PHASE(1);
+    {
+      uint32_t h[8];
+      sc_reduce512(h, hram);
+      sc_lattice_reduce(lat, h);
+    }
+    SV_PHASE(2);
+    sv_build_ltab(tabA, negA);
+    sv_build_ltab(tabR, negR);
+    SV_PHASE(3);
+#else
+    bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR);
+#endif
+    const int wl = sv_lat_windows(lat.bits);
+    int W = SV_LAT_MIN_WINDOWS;
+    while (__ballot(wl > W) != 0) ++W;
+    W = __builtin_amdgcn_readfirstlane(W);
+    sv_lat_digits D;
+    sv_lat_prepare(D, lat, S, W);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // table stores before the DMA reads
+    SV_PHASE(4);
+    ge_p3 P;
+    sv_lat_scalarmult<true>(P, D, W, tabA, tabR, btab0, btab1, stage);
+    SV_PHASE(5);
+    ok = ok && sv_is_identity(P) && active;
+    SV_PHASE(6);
+    if (active) p.verdict[i] = ok ? 1 : 0;
+    const uint64_t mask = __ballot(ok);
+    if (p.bitmap != nullptr && lane == 0) p.bitmap[base >> 6] = mask;
+  }
+}
+
 __global__ void sv_btab_init_kernel(uint32_t* btab) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < SV_BTAB_ENTRIES) sv_btab_entry(btab + e * SV_BTAB_STRIDE, e);
+#if SV_LATTICE
+  else if (e < 2 * SV_BTAB_ENTRIES)
+    sv_btab_entry_shift(btab + e * SV_BTAB_STRIDE, e - SV_BTAB_ENTRIES, 128);
+#endif
 }
 
 struct sv_sparams {
@@ -182,20 +274,36 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_sign_kernel(sv
 // ------------------------------------------------------------ launchers
 extern "C" {
 
+#ifdef SV_PHASE_PROF
+int sv_debug_phase_cycles(unsigned long long out[8], int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sv_phase_cycles), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(sv_phase_cycles), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
 size_t sv_ws_bytes_per_block(void) { return (size_t)SV_BLOCK * SV_SLOT_QUADS * sizeof(sv_u4); }
-size_t sv_btab_bytes(void) { return (size_t)SV_BTAB_DWORDS * 4; }
+size_t sv_btab_bytes(void) { return (size_t)SV_NBTAB * SV_BTAB_DWORDS * 4; }
 int sv_block_threads(void) { return SV_BLOCK; }
 
 hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s) {
-  hipLaunchKernelGGL(sv_btab_init_kernel, dim3((SV_BTAB_ENTRIES + 191) / 192), dim3(192), 0, s, d_btab);
+  hipLaunchKernelGGL(sv_btab_init_kernel, dim3((SV_NBTAB * SV_BTAB_ENTRIES + 191) / 192), dim3(192), 0, s, d_btab);
   return hipGetLastError();
 }
 
 int sv_occupancy_blocks_per_cu(void) {
   int b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, sv_verify_kernel<0>, SV_BLOCK, 0) != hipSuccess) b0 = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, sv_verify_kernel<1>, SV_BLOCK, 0) != hipSuccess) b1 = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, sv_verify_kernel<2>, SV_BLOCK, 0) != hipSuccess) b2 = 1;
+#if SV_LATTICE
+#define SV_VK sv_verify_lat_kernel
+#else
+#define SV_VK sv_verify_kernel
+#endif
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, SV_VK<0>, SV_BLOCK, 0) != hipSuccess) b0 = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, SV_VK<1>, SV_BLOCK, 0) != hipSuccess) b1 = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, SV_VK<2>, SV_BLOCK, 0) != hipSuccess) b2 = 1;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b3, sv_sign_kernel, SV_BLOCK, 0) != hipSuccess) b3 = 1;
   int m = b0;
   if (b1 > m) m = b1;
@@ -219,12 +327,21 @@ hipError_t sv_launch_verify(int mode, unsigned grid, const void* pk, const void*
   p.bitmap = (uint64_t*)bitmap;
   p.ws = (sv_u4*)ws;
   p.btab = (const sv_u4*)btab;
+#if SV_LATTICE
+  if (mode == 0)
+    hipLaunchKernelGGL(sv_verify_lat_kernel<0>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
+  else if (mode == 1)
+    hipLaunchKernelGGL(sv_verify_lat_kernel<1>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
+  else
+    hipLaunchKernelGGL(sv_verify_lat_kernel<2>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
+#else
   if (mode == 0)
     hipLaunchKernelGGL(sv_verify_kernel<0>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
   else if (mode == 1)
     hipLaunchKernelGGL(sv_verify_kernel<1>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
   else
     hipLaunchKernelGGL(sv_verify_kernel<2>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
+#endif
   return hipGetLastError();
 }
 

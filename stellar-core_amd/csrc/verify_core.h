@@ -25,6 +25,7 @@
 #pragma once
 
 #include "ge25519.h"
+#include "lattice.h"
 #include "sc25519.h"
 #include "sha512_dev.h"
 
@@ -55,7 +56,13 @@ struct __attribute__((aligned(16))) sv_u4 {
 // and the per-lane workspace slot: table_A + K pending points (X, Y, Z).
 #define SV_BATCH_K 4
 #define SV_PEND_QUADS 9
-#define SV_SLOT_QUADS (SV_ATAB_ENTRIES * SV_ATAB_QUADS + SV_BATCH_K * SV_PEND_QUADS)
+#define SV_SLOT_QUADS_W (SV_ATAB_ENTRIES * SV_ATAB_QUADS + SV_BATCH_K * SV_PEND_QUADS)
+// Half-size path (lattice.h): tables of -A and -R, 9 entries x 10 quads each
+// (YpX, YmX, Z, T2d as 4 x 10 dwords back to back; a negative digit swaps
+// YpX/YmX by select after the load).
+#define SV_LTAB_QUADS 10
+#define SV_SLOT_QUADS_L (2 * SV_ATAB_ENTRIES * SV_LTAB_QUADS)
+#define SV_SLOT_QUADS (SV_SLOT_QUADS_W > SV_SLOT_QUADS_L ? SV_SLOT_QUADS_W : SV_SLOT_QUADS_L)
 
 SV_HD bool sv_small_order(const uint32_t s[8]) {
   const uint32_t bl[7][8] = {
@@ -450,4 +457,247 @@ SV_HD void sv_sign_lane(uint32_t pk[8], uint32_t sig[16], const uint32_t seed[8]
   uint32_t S[8];
   sc_muladd(S, h, a, r);
   SV_UNROLL for (int i = 0; i < 8; ++i) { sig[i] = enc[i]; sig[8 + i] = S[i]; }
+}
+
+// ------------------------------------------------ half-size path (lattice.h)
+// Base-point tables for the half-size path: entry e of table t is e·(2^(128 t) B)
+// (t = 0, 1), same 36-dword affine precomp layout as table_B.
+SV_HD void sv_btab_entry_shift(uint32_t out[SV_BTAB_STRIDE], int e, int shift) {
+  const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                            0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+  ge_p3 B, acc;
+  ge_frombytes(B, benc, false);
+  ge_p1p1 Q;
+  for (int i = 0; i < shift; ++i) {
+    ge_dbl(Q, B.X, B.Y, B.Z);
+    ge_p1p1_to_p3(B, Q);
+  }
+  ge_cached bc;
+  ge_p3_to_cached(bc, B);
+  fe_0(acc.X); fe_1(acc.Y); fe_1(acc.Z); fe_0(acc.T);
+  for (int bit = 15; bit >= 0; --bit) {
+    ge_dbl(Q, acc.X, acc.Y, acc.Z);
+    ge_p1p1_to_p3(acc, Q);
+    if ((e >> bit) & 1) {
+      ge_add_preswapped(Q, acc, bc.YpX, bc.YmX, bc.Z, bc.T2d, false, false);
+      ge_p1p1_to_p3(acc, Q);
+    }
+  }
+  fe zi, x, y, xy, d2, ypx, ymx, xy2d;
+  fe_invert(zi, acc.Z);
+  fe_mul(x, acc.X, zi);
+  fe_mul(y, acc.Y, zi);
+  fe_mul(xy, x, y);
+  fe_const_2d(d2);
+  fe_mul(xy2d, xy, d2);
+  fe_add(ypx, y, x);
+  fe_weak(ypx);
+  fe_sub(ymx, y, x);
+  fe_weak(ymx);
+  for (int i = 0; i < SV_BTAB_STRIDE; ++i) out[i] = 0;
+  for (int i = 0; i < 10; ++i) {
+    out[i] = ypx.v[i];
+    out[12 + i] = ymx.v[i];
+    out[24 + i] = xy2d.v[i];
+  }
+}
+
+// cached entry as 40 packed dwords (10 quads): YpX YmX Z T2d
+SV_HD void sv_store_lentry(sv_u4* p, const ge_cached& c) {
+  uint32_t w[40];
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    w[i] = c.YpX.v[i];
+    w[10 + i] = c.YmX.v[i];
+    w[20 + i] = c.Z.v[i];
+    w[30 + i] = c.T2d.v[i];
+  }
+  SV_UNROLL for (int q = 0; q < 10; ++q) p[q] = sv_u4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+}
+// loads an entry with a digit's sign applied: (qa, qb) = (YpX, YmX) or swapped
+SV_HD void sv_load_lentry(fe& qa, fe& qb, fe& qz, fe& qt, const sv_u4* p, int qstride, bool neg) {
+  uint32_t w[40];
+  SV_UNROLL for (int q = 0; q < 10; ++q) {
+    const sv_u4 v = p[q * qstride];
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    qa.v[i] = neg ? w[10 + i] : w[i];
+    qb.v[i] = neg ? w[i] : w[10 + i];
+    qz.v[i] = w[20 + i];
+    qt.v[i] = w[30 + i];
+  }
+}
+
+// {0..8}·P in cached form into tab (9 entries x 10 quads, lane-contiguous)
+SV_COLD void sv_build_ltab(sv_u4* tab, const ge_p3& P) {
+  ge_cached c1, ce;
+  ge_p3_to_cached(c1, P);
+  ge_cached_identity(ce);
+  sv_store_lentry(tab, ce);
+  sv_store_lentry(tab + SV_LTAB_QUADS, c1);
+  ge_p3 P3 = P;
+  ge_p1p1 Q;
+  SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
+    ge_add_preswapped(Q, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, false);
+    ge_p1p1_to_p3(P3, Q);
+    ge_p3_to_cached(ce, P3);
+    sv_store_lentry(tab + e * SV_LTAB_QUADS, ce);
+  }
+}
+
+// Shifts a packed signed radix-16 digit string (64 digits) left by k digits.
+SV_HD void sv_digits_shift(uint32_t d[8], int k) {
+  SV_NOUNROLL while (k >= 8) {
+    SV_UNROLL for (int i = 7; i > 0; --i) d[i] = d[i - 1];
+    d[0] = 0;
+    k -= 8;
+  }
+  SV_NOUNROLL for (; k > 0; --k) (void)sc_pop_top(d, 4);
+}
+
+// Per-signature digit strings of (*) in lattice.h for W windows:
+//   dA: c0, dR: |c1| (signed radix 16, top digit = window W-1),
+//   dB[j] = digit j of (s mod 2^128) | digit j of (s >> 128) << 16 (radix 2^16,
+//   j = 0..8; digit j is added at window 4j).
+// A scalar of 4W-1 bits can carry out of digit W-1: that digit is then -8 and
+// the carry is 1, i.e. the top digit is really +8 (table entries go to 8);
+// top8A / top8R record it (4-bit two's complement digits stop at 7).
+struct sv_lat_digits {
+  uint32_t dA[8], dR[8], dB[9];
+  bool rneg, top8A, top8R;
+};
+
+SV_COLD void sv_lat_prepare(sv_lat_digits& D, const sv_lat& lat, const uint32_t S[8], int W) {
+  sc_digits_r16(D.dA, lat.c0);
+  sc_digits_r16(D.dR, lat.c1);
+  if (W < 64) {  // (W = 64 only for full-length scalars < 2^253: no carry out)
+    sv_digits_shift(D.dA, 63 - W);
+    sv_digits_shift(D.dR, 63 - W);
+    D.top8A = sc_pop_top(D.dA, 4) != 0;  // digit W: the carry
+    D.top8R = sc_pop_top(D.dR, 4) != 0;
+  } else {
+    D.top8A = D.top8R = false;
+  }
+  D.rneg = lat.c1neg;
+  uint32_t s[8], lo[8], hi[8], d0[8], d1[8];
+  sc_mul_signed(s, lat.c1, lat.c1neg, S);
+  SV_UNROLL for (int i = 0; i < 8; ++i) {
+    lo[i] = i < 4 ? s[i] : 0u;
+    hi[i] = i < 4 ? s[4 + i] : 0u;
+  }
+  sc_digits_r65536(d0, lo);
+  sc_digits_r65536(d1, hi);
+  SV_UNROLL for (int j = 0; j < 9; ++j) {
+    const uint32_t a = (d0[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+    const uint32_t b = (d1[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+    D.dB[j] = a | (b << 16);
+  }
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// LDS-DMA of one lane-contiguous 10-quad table entry into a lane-linear stage
+SV_HD void sv_stage_lentry(sv_u4* stage, const sv_u4* entry) {
+  SV_UNROLL for (int q = 0; q < SV_LTAB_QUADS; ++q)
+    __builtin_amdgcn_global_load_lds((const void*)(entry + q), (__attribute__((address_space(3))) void*)(stage + q * 64),
+                                     16, 0, 0);
+}
+#endif
+
+// P' = [s]B + [c0](-A) + [c1](-R) over W windows (MSB first).  tabA / tabR:
+// the lane's tables of -A / -R; btab0 / btab1: e·B / e·(2^128 B).
+// Step machine per window w: s = 0..3 doubling (skipped in the top window,
+// where P is the identity), s = 4 add tabA[dA], s = 5 add tabR[+-dR], and on
+// windows w = 4j, j <= 8: s = 6 add btab0[dB0_j], s = 7 add btab1[dB1_j].
+// STAGED (device): the window's A and R entries are DMA'd into the wave's LDS
+// stage (2 x 10 quads x 64 lanes) when the window starts.
+template <bool STAGED = false>
+SV_HD void sv_lat_scalarmult(ge_p3& P, sv_lat_digits& D, int W, const sv_u4* tabA, const sv_u4* tabR,
+                             const sv_u4* btab0, const sv_u4* btab1, sv_u4* stage = nullptr) {
+  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
+  ge_p1p1 Q;
+  SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
+    int32_t dA = sc_pop_top(D.dA, 4);
+    int32_t dR = sc_pop_top(D.dR, 4);
+    if (w == W - 1) {
+      if (D.top8A) dA = 8;
+      if (D.top8R) dR = 8;
+    }
+    if (D.rneg) dR = -dR;
+    const bool bwin = (w & 3) == 0 && (w >> 2) <= 8;
+    int32_t dB0 = 0, dB1 = 0;
+    if (bwin) {
+      const uint32_t t = D.dB[8];
+      dB0 = ((int32_t)(t << 16)) >> 16;
+      dB1 = ((int32_t)t) >> 16;
+      SV_UNROLL for (int i = 8; i > 0; --i) D.dB[i] = D.dB[i - 1];
+      D.dB[0] = 0;
+    }
+    const int nsteps = bwin ? 8 : 6;
+    const int s0 = (w == W - 1) ? 4 : 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (STAGED) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      sv_stage_lentry(stage, tabA + (dA < 0 ? -dA : dA) * SV_LTAB_QUADS);
+      sv_stage_lentry(stage + SV_LTAB_QUADS * 64, tabR + (dR < 0 ? -dR : dR) * SV_LTAB_QUADS);
+    }
+#endif
+    SV_NOUNROLL for (int s = s0; s < nsteps; ++s) {
+      if (s < 4) {
+        ge_dbl(Q, P.X, P.Y, P.Z);
+      } else {
+        fe qa, qb, qz, qt;
+        bool neg;
+        const bool zone = s >= 6;
+        if (!zone) {
+          const int32_t d = s == 4 ? dA : dR;
+          neg = d < 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+          if (STAGED) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            sv_load_lentry(qa, qb, qz, qt, stage + (s == 4 ? 0 : SV_LTAB_QUADS * 64) + __lane_id(), 64, neg);
+          } else
+#endif
+          {
+            const sv_u4* e = (s == 4 ? tabA : tabR) + (neg ? -d : d) * SV_LTAB_QUADS;
+            sv_load_lentry(qa, qb, qz, qt, e, 1, neg);
+          }
+        } else {
+          const int32_t d = s == 6 ? dB0 : dB1;
+          neg = d < 0;
+          fe_1(qz);
+          const sv_u4* e = (s == 6 ? btab0 : btab1) + (neg ? -d : d) * SV_BTAB_QUADS;
+          sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
+          sv_load_fe3(qb, e + (neg ? 0 : 3), 1);
+          sv_load_fe3(qt, e + 6, 1);
+        }
+        ge_add_preswapped(Q, P, qa, qb, qz, qt, neg, zone);
+      }
+      ge_p1p1_to_p3_opt(P, Q, s + 1 >= 4 && s + 1 < nsteps);
+    }
+  }
+}
+
+// P' == identity: X == 0 and Y == Z (mod p)
+SV_HD bool sv_is_identity(const ge_p3& P) {
+  fe d;
+  fe_sub(d, P.Y, P.Z);
+  return fe_iszero(P.X) && fe_iszero(d);
+}
+
+// Steps (1)-(5) of libsodium plus the decode of R (lattice.h), the Euclid
+// reduction and the table build.  Returns the pre-verdict and the lane's
+// window count in *W_lane; the caller picks the wave's W >= every W_lane.
+SV_COLD bool sv_lat_pre(sv_lat& lat, const uint32_t A[8], const uint32_t R[8], const uint32_t S[8],
+                        const uint32_t hram[16], sv_u4* tabA, sv_u4* tabR) {
+  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
+            sv_point_canonical(R);
+  ge_p3 negA, negR;
+  ok = ge_frombytes(negA, A, true) && ok;
+  ok = ge_frombytes(negR, R, true) && ok;
+  uint32_t h[8];
+  sc_reduce512(h, hram);
+  sc_lattice_reduce(lat, h);
+  sv_build_ltab(tabA, negA);
+  sv_build_ltab(tabR, negR);
+  return ok;
 }

@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../stellar-core_amd/csrc/verify_core.h"
@@ -13,9 +14,21 @@
 static std::vector<uint32_t> g_btab;
 static std::once_flag g_once;
 
+static std::vector<uint32_t> g_btab1;  // e·(2^128 B) for the half-size path
+
 static void init_btab() {
   g_btab.assign(SV_BTAB_DWORDS + 8, 0);
-  for (int e = 0; e < SV_BTAB_ENTRIES; ++e) sv_btab_entry(&g_btab[e * SV_BTAB_STRIDE], e);
+  g_btab1.assign(SV_BTAB_DWORDS + 8, 0);
+  // (the build container has 8 CPUs; the tables are test setup only)
+  std::vector<std::thread> th;
+  for (int t = 0; t < 8; ++t)
+    th.emplace_back([t] {
+      for (int e = t; e < SV_BTAB_ENTRIES; e += 8) {
+        sv_btab_entry(&g_btab[e * SV_BTAB_STRIDE], e);
+        sv_btab_entry_shift(&g_btab1[e * SV_BTAB_STRIDE], e, 128);
+      }
+    });
+  for (auto& x : th) x.join();
 }
 
 static void load_words(uint32_t w[8], const uint8_t* b) { memcpy(w, b, 32); }
@@ -164,6 +177,47 @@ void hc_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, 
     verdict[i] = sv_verify_core(A, (const sv_u4*)R, S, hram, slot.data(), 1, (const sv_u4*)g_btab.data()) ? 1 : 0;
   }
 }
+}
+
+// Half-size (lattice.h) per-lane verifier.  wmin forces at least that many
+// windows (the kernel runs every lane of a wave at the wave's maximum), so
+// tests can check that verdicts do not depend on W.  stats (optional, n ints):
+// the lane's own window count.
+extern "C" void hc_verify_batch_lat(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                                    const uint32_t* len, size_t n, uint8_t* verdict, int wmin, int32_t* stats) {
+  std::call_once(g_once, init_btab);
+  std::vector<sv_u4> slot(SV_SLOT_QUADS_L);
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t A[8], R[8], S[8], hram[16];
+    load_words(A, pk + 32 * i);
+    load_words(R, sig + 64 * i);
+    load_words(S, sig + 64 * i + 32);
+    sha512_ram_var(hram, R, A, msg + off[i], len[i]);
+    sv_lat lat;
+    sv_u4* tabA = slot.data();
+    sv_u4* tabR = tabA + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
+    const bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR);
+    int W = sv_lat_windows(lat.bits);
+    if (stats) stats[i] = W;
+    if (W < wmin) W = wmin;
+    sv_lat_digits D;
+    sv_lat_prepare(D, lat, S, W);
+    ge_p3 P;
+    sv_lat_scalarmult(P, D, W, tabA, tabR, (const sv_u4*)g_btab.data(), (const sv_u4*)g_btab1.data());
+    verdict[i] = (ok && sv_is_identity(P)) ? 1 : 0;
+  }
+}
+
+// Euclid reduction only: c0, |c1| as 8 words each, c1neg, bits.
+extern "C" int hc_lattice_reduce(const uint8_t h[32], uint8_t c0[32], uint8_t c1[32], int* c1neg) {
+  uint32_t hw[8];
+  load_words(hw, h);
+  sv_lat lat;
+  sc_lattice_reduce(lat, hw);
+  memcpy(c0, lat.c0, 32);
+  memcpy(c1, lat.c1, 32);
+  *c1neg = lat.c1neg ? 1 : 0;
+  return lat.bits;
 }
 
 // Engine stubs for timing the host mirror's own bookkeeping (no crypto):

@@ -55,7 +55,7 @@ def _gpu_sign(sv, dev, seeds, msgs):
     return tpk, tsig, tm
 
 
-@pytest.mark.parametrize("name", ["intree", "valid", "msglen", "adversarial"])
+@pytest.mark.parametrize("name", ["intree", "valid", "msglen", "adversarial", "lattice_edge"])
 def test_golden_fixtures_variable_path(sv, dev, golden, name):
     d = golden[name]
     out = sv.verify_batch(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"], device=0)
@@ -73,7 +73,7 @@ def test_intree_reference_expectations(sv, dev, golden):
 
 
 def test_fixed32_path_on_golden_rows(sv, dev, golden):
-    for name in ("valid", "adversarial"):
+    for name in ("valid", "adversarial", "lattice_edge"):
         d = golden[name]
         rows = np.nonzero(d["msg_len"] == 32)[0]
         msgs = np.stack([d["msg"][o:o + 32] for o in d["msg_off"][rows]])

@@ -213,3 +213,72 @@ def test_device_sha256(hostcore):
         assert out.raw == hashlib.sha256(buf[pad:pad + n]).digest(), n
     hostcore.hc_sha256(out, b"abc", 3)  # FIPS 180-2 appendix B.1
     assert out.raw.hex() == "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"
+
+
+# ------------------------------------------------ half-size path (lattice.h)
+N8 = 8 * L
+
+
+def test_lattice_reduce_invariants(hostcore):
+    """c0 == c1 h (mod 8L), c1 odd, reported bit length exact, short for random h;
+    degenerate h fall back to the trivial pair (h, 1)."""
+    c0 = ctypes.create_string_buffer(32)
+    c1 = ctypes.create_string_buffer(32)
+    neg = ctypes.c_int()
+    rnd = random.Random(17)
+    hs = [0, 1, 2, 7, 8, L - 1, L - 8, 2**128 - 1, 2**128, 2**128 + 1, 2**252, (L - 1) // 8] + \
+        [rnd.randrange(L) for _ in range(4000)]
+    long_pairs = 0
+    for h in hs:
+        nb = hostcore.hc_lattice_reduce(h.to_bytes(32, "little"), c0, c1, ctypes.byref(neg))
+        a = int.from_bytes(c0.raw, "little")
+        b = int.from_bytes(c1.raw, "little")
+        b = -b if neg.value else b
+        assert (a - b * h) % N8 == 0 and b % 2 == 1 and a >= 0, h
+        assert nb == max(a.bit_length(), abs(b).bit_length(), 1), h
+        long_pairs += nb > 135
+    assert long_pairs <= 12  # only the hand-picked degenerate h need long pairs
+
+
+def _host_verify_lat(hostcore, d, rows, wmin=0):
+    pk = np.ascontiguousarray(d["pk"][rows])
+    sig = np.ascontiguousarray(d["sig"][rows])
+    msg = np.ascontiguousarray(d["msg"])
+    off = np.ascontiguousarray(d["msg_off"][rows])
+    ln = np.ascontiguousarray(d["msg_len"][rows])
+    out = np.zeros(len(rows), np.uint8)
+    wins = np.zeros(len(rows), np.int32)
+    hostcore.hc_verify_batch_lat(ctypes.c_void_p(pk.ctypes.data), ctypes.c_void_p(sig.ctypes.data),
+                                 ctypes.c_void_p(msg.ctypes.data), ctypes.c_void_p(off.ctypes.data),
+                                 ctypes.c_void_p(ln.ctypes.data), ctypes.c_size_t(len(rows)),
+                                 ctypes.c_void_p(out.ctypes.data), ctypes.c_int(wmin),
+                                 ctypes.c_void_p(wins.ctypes.data))
+    return out, wins
+
+
+def test_lattice_lane_verifier_matches_golden(hostcore, golden):
+    """The half-size equation gives libsodium's verdict on every fixture class,
+    incl. mixed-order keys, torsion in both A and R, and the digit-carry edge
+    (pairs of exactly 4W-1 bits)."""
+    for name, d in golden.items():
+        rows = np.arange(len(d["verdict"]))
+        if name in ("adversarial", "valid"):
+            rows = rows[1::3]
+        got, wins = _host_verify_lat(hostcore, d, rows)
+        bad = np.nonzero(got != d["verdict"][rows])[0]
+        assert len(bad) == 0, (name, [str(d["class_names"][d["cls"][rows[i]]]) for i in bad[:10]])
+        assert wins.min() >= 33 and wins.max() <= 64
+    e = golden["lattice_edge"]
+    _, wins = _host_verify_lat(hostcore, e, np.arange(len(e["verdict"])))
+    assert (wins >= 34).any()  # the W = 34 class is really exercised
+
+
+def test_lattice_verdicts_independent_of_window_count(hostcore, golden):
+    """A wave runs every lane at the wave's maximum W: extra all-zero top windows
+    must not change any verdict (W = 64 is the full-length fallback)."""
+    for name in ("lattice_edge", "intree"):
+        d = golden[name]
+        rows = np.arange(len(d["verdict"]))
+        for wmin in (34, 41, 64):
+            got, _ = _host_verify_lat(hostcore, d, rows, wmin)
+            assert np.array_equal(got, d["verdict"][rows]), (name, wmin)

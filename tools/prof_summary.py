@@ -14,6 +14,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -27,7 +28,7 @@ def main():
     ks = glob.glob(os.path.join(d, "kt", "*_kernel_stats.csv"))
     if ks:
         for r in csv.DictReader(open(ks[0])):
-            if "sv_verify_kernel" in r["Name"]:
+            if re.search(r"sv_verify(_lat)?_kernel<0>", r["Name"]):
                 out["kernel"] = r["Name"]
                 out["calls"] = int(r["Calls"])
                 out["avg_ns"] = float(r["AverageNs"])
@@ -37,7 +38,7 @@ def main():
     meta = {}
     for f in glob.glob(os.path.join(d, "*", "*_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "sv_verify_kernel<0>" not in r["Kernel_Name"]:
+            if not re.search(r"sv_verify(_lat)?_kernel<0>", r["Kernel_Name"]):
                 continue
             if int(r["Grid_Size"]) < 1024:
                 continue
