@@ -128,20 +128,51 @@ SV_HD void fe_carry_wide(fe& out, uint64_t h[10]) {
 #ifndef SV_MAD_ASM
 #define SV_MAD_ASM 1
 #endif
-SV_HD void sv_mad_init(uint64_t& acc, uint32_t a, uint32_t b) {
+// Carry-out SGPR pairs the inline-asm mads rotate over (SV_MAD_PAIRS > 0):
+// a VALU write of the SAME SGPR pair by consecutive mads serialises them
+// (tools/ubench_valu.hip: 9.5 vs 6.4 cycles per wave-instruction at one wave
+// per SIMD), so product k writes pair k mod SV_MAD_PAIRS from the top of the
+// SGPR file (never read; declared clobbered so the allocator avoids them).
+#ifndef SV_MAD_PAIRS
+#define SV_MAD_PAIRS 4
+#endif
+// (k must fold to a constant: every caller is a fully unrolled loop)
+SV_HD void sv_mad_init_k(uint64_t& acc, uint32_t a, uint32_t b, int k) {
 #if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
-  asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "vcc");
+#if SV_MAD_PAIRS > 0
+  k %= SV_MAD_PAIRS;
+  if (k == 0) asm("v_mad_u64_u32 %0, s[94:95], %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "s94", "s95");
+  else if (k == 1) asm("v_mad_u64_u32 %0, s[92:93], %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "s92", "s93");
+  else if (k == 2) asm("v_mad_u64_u32 %0, s[90:91], %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "s90", "s91");
+  else asm("v_mad_u64_u32 %0, s[88:89], %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "s88", "s89");
 #else
+  (void)k;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "vcc");
+#endif
+#else
+  (void)k;
   acc = (uint64_t)a * b;
 #endif
 }
-SV_HD void sv_mad(uint64_t& acc, uint32_t a, uint32_t b) {
+SV_HD void sv_mad_k(uint64_t& acc, uint32_t a, uint32_t b, int k) {
 #if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
-  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
+#if SV_MAD_PAIRS > 0
+  k %= SV_MAD_PAIRS;
+  if (k == 0) asm("v_mad_u64_u32 %0, s[94:95], %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "s94", "s95");
+  else if (k == 1) asm("v_mad_u64_u32 %0, s[92:93], %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "s92", "s93");
+  else if (k == 2) asm("v_mad_u64_u32 %0, s[90:91], %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "s90", "s91");
+  else asm("v_mad_u64_u32 %0, s[88:89], %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "s88", "s89");
 #else
+  (void)k;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
+#endif
+#else
+  (void)k;
   acc += (uint64_t)a * b;
 #endif
 }
+SV_HD void sv_mad_init(uint64_t& acc, uint32_t a, uint32_t b) { sv_mad_init_k(acc, a, b, 0); }
+SV_HD void sv_mad(uint64_t& acc, uint32_t a, uint32_t b) { sv_mad_k(acc, a, b, 0); }
 
 // Column sums of f*g (DBL: of 2*f*g).  Wrapped columns (i+j >= 10) carry the
 // factor 2^255 = 19 on g; odd*odd products carry an extra 2 (half-bit radix).
@@ -158,14 +189,14 @@ SV_HD void fe_mul_cols(uint64_t h[10], const fe& f, const fe& g) {
       const int k = i + j;
       const uint32_t a = ((i & 1) && (j & 1)) ? fb[i] : fa[i];
       const uint32_t b = (k >= 10) ? g19[j] : g.v[j];
-      if (i == 0) sv_mad_init(h[k], a, b);  // i == 0 opens every column
-      else sv_mad(h[k >= 10 ? k - 10 : k], a, b);
+      if (i == 0) sv_mad_init_k(h[k], a, b, 10 * i + j);  // i == 0 opens every column
+      else sv_mad_k(h[k >= 10 ? k - 10 : k], a, b, 10 * i + j);
     }
   }
 }
 
 #ifndef SV_SQ_ASM
-#define SV_SQ_ASM 0
+#define SV_SQ_ASM 1
 #endif
 // Column sums of f^2 (DBL: 2 f^2), using the symmetry f_i f_j = f_j f_i.
 template <bool DBL>
@@ -177,8 +208,8 @@ SV_HD void fe_sq_cols(uint64_t h[10], const fe& f) {
       const uint32_t a = f.v[i] << sh;
       const uint32_t b = (k >= 10) ? 19u * f.v[j] : f.v[j];
 #if SV_SQ_ASM
-      if (i == 0) sv_mad_init(h[k], a, b);
-      else sv_mad(h[k >= 10 ? k - 10 : k], a, b);
+      if (i == 0) sv_mad_init_k(h[k], a, b, 10 * i + j);
+      else sv_mad_k(h[k >= 10 ? k - 10 : k], a, b, 10 * i + j);
 #else
       // plain C here: squaring operands are never phi-merged, so LLVM keeps
       // them 32-bit, and compiler-emitted mads need no hazard s_nops

@@ -594,6 +594,11 @@ SV_COLD void sv_lat_prepare(sv_lat_digits& D, const sv_lat& lat, const uint32_t 
   }
 }
 
+// 1: the window's two base-point entries are also staged by LDS-DMA (into the
+// A and R regions once those entries have been read)
+#ifndef SV_LAT_STAGE_B
+#define SV_LAT_STAGE_B 1
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 // LDS-DMA of one lane-contiguous 10-quad table entry into a lane-linear stage
 SV_HD void sv_stage_lentry(sv_u4* stage, const sv_u4* entry) {
@@ -653,8 +658,17 @@ SV_HD void sv_lat_scalarmult(ge_p3& P, sv_lat_digits& D, int W, const sv_u4* tab
           neg = d < 0;
 #if defined(__HIP_DEVICE_COMPILE__)
           if (STAGED) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            sv_load_lentry(qa, qb, qz, qt, stage + (s == 4 ? 0 : SV_LTAB_QUADS * 64) + __lane_id(), 64, neg);
+            // s = 4: the A and R entries (DMA'd at window start) have landed
+            if (s == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            sv_u4* reg = stage + (s == 4 ? 0 : SV_LTAB_QUADS * 64);
+            sv_load_lentry(qa, qb, qz, qt, reg + __lane_id(), 64, neg);
+            if (SV_LAT_STAGE_B && bwin) {
+              // this region is free once its reads retire: stage the B entry
+              // that step s + 2 adds (B0 into A's region, B1 into R's)
+              const int32_t db = s == 4 ? dB0 : dB1;
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              sv_stage_bentry(reg, s == 4 ? btab0 : btab1, db);
+            }
           } else
 #endif
           {
@@ -665,10 +679,23 @@ SV_HD void sv_lat_scalarmult(ge_p3& P, sv_lat_digits& D, int W, const sv_u4* tab
           const int32_t d = s == 6 ? dB0 : dB1;
           neg = d < 0;
           fe_1(qz);
-          const sv_u4* e = (s == 6 ? btab0 : btab1) + (neg ? -d : d) * SV_BTAB_QUADS;
-          sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
-          sv_load_fe3(qb, e + (neg ? 0 : 3), 1);
-          sv_load_fe3(qt, e + 6, 1);
+#if defined(__HIP_DEVICE_COMPILE__)
+          if (STAGED && SV_LAT_STAGE_B) {
+            // B0's DMA is older than B1's 9: vmcnt(9) covers it
+            if (s == 6) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const sv_u4* st = stage + (s == 6 ? 0 : SV_LTAB_QUADS * 64) + __lane_id();
+            sv_load_fe3(qa, st, 64);
+            sv_load_fe3(qb, st + 3 * 64, 64);
+            sv_load_fe3(qt, st + 6 * 64, 64);
+          } else
+#endif
+          {
+            const sv_u4* e = (s == 6 ? btab0 : btab1) + (neg ? -d : d) * SV_BTAB_QUADS;
+            sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
+            sv_load_fe3(qb, e + (neg ? 0 : 3), 1);
+            sv_load_fe3(qt, e + 6, 1);
+          }
         }
         ge_add_preswapped(Q, P, qa, qb, qz, qt, neg, zone);
       }
