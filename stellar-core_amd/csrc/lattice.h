@@ -34,10 +34,16 @@
 // >= 2^32) falls back to the trivial pair (h, 1), which is (*) with the full
 // 253-bit scalar: correct, only slower for its wave.
 //
-// Quotients are estimated in double precision and always UNDER-estimated, so
-// every step is an exact integer step of the same Euclidean sequence (a short
-// estimate only splits one quotient over two iterations).
+// The Euclid runs as Lehmer steps (sv_lehmer_step): ~12 quotients at a time on
+// the leading 53 bits in exact double arithmetic, then one 2x2 matrix applied
+// to the 256-bit pair -- about 6 matrix applications and one exact step per
+// signature instead of ~75 exact 256-bit steps (-2.9 % kernel time measured).
+// The exact steps estimate their quotient in double precision and always
+// UNDER-estimate it, so each is an exact integer step of the same Euclidean
+// sequence (a short estimate only splits one quotient over two iterations).
 #pragma once
+
+#include <math.h>
 
 #include "sc25519.h"
 
@@ -104,6 +110,113 @@ struct sv_lat {
 #define SV_LAT_SPLIT_WORDS 4  // Euclid stops at the first remainder < 2^(32 * 4)
 #define SV_LAT_MAX_ITERS 400  // > 1.45 * 256 (worst-case Euclid length)
 
+// 1: Lehmer steps (below); 0: one 256-bit step per quotient only.
+#ifndef SV_LEHMER
+#define SV_LEHMER 1
+#endif
+
+// d = u*x - v*y over 8 words (u, v < 2^32); returns true iff the exact value
+// is negative (the values combined here are always within (-2^256, 2^256)).
+SV_HD bool sv_lincomb8(uint32_t d[8], uint32_t u, const uint32_t x[8], uint32_t v, const uint32_t y[8]) {
+  uint64_t cx = 0, cy = 0;
+  uint32_t br = 0;
+  SV_UNROLL for (int i = 0; i < 8; ++i) {
+    const uint64_t px = (uint64_t)u * x[i] + cx;
+    const uint64_t py = (uint64_t)v * y[i] + cy;
+    cx = px >> 32;
+    cy = py >> 32;
+    const uint64_t t = (uint64_t)(uint32_t)px - (uint32_t)py - br;
+    d[i] = (uint32_t)t;
+    br = (uint32_t)(t >> 63);
+  }
+  return (int64_t)cx - (int64_t)cy - (int64_t)br < 0;
+}
+
+// d = u*x + v*y (mod 2^256), u, v < 2^30
+SV_HD void sv_addcomb8(uint32_t d[8], uint32_t u, const uint32_t x[8], uint32_t v, const uint32_t y[8]) {
+  uint64_t c = 0;
+  SV_UNROLL for (int i = 0; i < 8; ++i) {
+    uint64_t t = (uint64_t)u * x[i] + c;
+    t += (uint64_t)v * y[i];
+    d[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+}
+
+// d = -d (two's complement) when neg
+SV_HD void sv_condneg8(uint32_t d[8], bool neg) {
+  const uint32_t m = neg ? 0xffffffffu : 0u;
+  uint32_t c = neg ? 1u : 0u;
+  SV_UNROLL for (int i = 0; i < 8; ++i) {
+    const uint64_t t = (uint64_t)(d[i] ^ m) + c;
+    d[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+}
+
+// Lehmer step (Knuth 4.5.2 Algorithm L, with Jebelean's a-priori test): runs
+// Euclid on the leading 53 bits of (a, b) in exact double arithmetic and
+// applies the accumulated 2x2 matrix to (a, b) and the cofactors once.
+//   A = a / 2^sh, B ~ b / 2^sh (integers < 2^53), |a - A 2^sh|, |b - B 2^sh| < 8 2^sh.
+//   After k steps r_k = (-1)^k (u_k A - v_k B) with u, v >= 0 (cofactor
+//   magnitudes add: the matrix has a checkerboard sign pattern for ANY
+//   quotients q >= 0), and the exact remainder with the same quotients is
+//   2^sh (r_k + e_k), |e_k| < 8 (u_k + v_k).  A step is taken only if
+//   r_{k+1} >= 8 (u_{k+1} + v_{k+1}) + 2^(128 - sh): then every exact remainder
+//   stays >= 2^128 > 0, so (a', b') >= 0 and the cofactors keep opposite signs,
+//   i.e. a' |tb'| + b' |ta'| = 8L still holds (the size bound the caller uses).
+//   A quotient that is off by one only costs progress, never correctness; the
+//   sign test after applying the matrix is a belt-and-braces guard.
+// Returns false (state unchanged) if no step could be taken.
+SV_HD bool sv_lehmer_step(uint32_t a[8], uint32_t b[8], uint32_t ta[8], uint32_t tb[8], bool& bneg) {
+  const double ad = sv_words_to_double(a), bd = sv_words_to_double(b);
+  int e;
+  (void)frexp(ad, &e);
+  const int sh = e - 53;  // a >= 2^128: sh >= 76
+  const double T = ldexp(1.0, 128 - sh);
+  double r0 = ldexp(ad, -sh), r1 = rint(ldexp(bd, -sh));
+  double u0 = 1.0, v0 = 0.0, u1 = 0.0, v1 = 1.0;
+  int k = 0;
+  SV_NOUNROLL for (; k < 48; ++k) {
+    double q = floor(r0 / r1);
+    double r2 = fma(-q, r1, r0);
+    if (r2 >= r1) {  // quotient rounded low
+      r2 -= r1;
+      q += 1.0;
+    }
+    const double u2 = fma(q, u1, u0), v2 = fma(q, v1, v0);
+    if (!(r2 >= 8.0 * (u2 + v2) + T)) break;  // (also catches r2 < 0)
+    r0 = r1;
+    r1 = r2;
+    u0 = u1;
+    v0 = v1;
+    u1 = u2;
+    v1 = v2;
+  }
+  if (k == 0) return false;
+  const uint32_t U0 = (uint32_t)u0, V0 = (uint32_t)v0, U1 = (uint32_t)u1, V1 = (uint32_t)v1;
+  const bool odd = (k & 1) != 0;
+  uint32_t na[8], nb[8];
+  bool nega = sv_lincomb8(na, U0, a, V0, b);  // a' = (-1)^k (u0 a - v0 b)
+  bool negb = sv_lincomb8(nb, U1, a, V1, b);  // b' = (-1)^(k+1) (u1 a - v1 b)
+  sv_condneg8(na, odd);
+  sv_condneg8(nb, !odd);
+  nega = nega != odd;
+  negb = negb == odd;
+  if (nega || negb) return false;  // (unreachable by the bound above)
+  uint32_t nta[8], ntb[8];
+  sv_addcomb8(nta, U0, ta, V0, tb);
+  sv_addcomb8(ntb, U1, ta, V1, tb);
+  SV_UNROLL for (int i = 0; i < 8; ++i) {
+    a[i] = na[i];
+    b[i] = nb[i];
+    ta[i] = nta[i];
+    tb[i] = ntb[i];
+  }
+  if (odd) bneg = !bneg;
+  return true;
+}
+
 // h < L (8 words).  Always returns a valid pair (falls back to (h, 1)).
 SV_COLD void sc_lattice_reduce(sv_lat& o, const uint32_t h[8]) {
   uint32_t a[8], b[8], ta[8], tb[8];
@@ -120,6 +233,22 @@ SV_COLD void sc_lattice_reduce(sv_lat& o, const uint32_t h[8]) {
     uint32_t hi = 0;
     SV_UNROLL for (int i = SV_LAT_SPLIT_WORDS; i < 8; ++i) hi |= b[i];
     if (hi == 0) break;
+#if SV_LEHMER
+    if (sv_lehmer_step(a, b, ta, tb, bneg)) {
+      if (sv_lt8(a, b)) {  // (a quotient rounded low)
+        SV_UNROLL for (int i = 0; i < 8; ++i) {
+          const uint32_t x = a[i], y = ta[i];
+          a[i] = b[i];
+          ta[i] = tb[i];
+          b[i] = x;
+          tb[i] = y;
+        }
+        bneg = !bneg;
+      }
+      continue;
+    }
+#endif
+    // one exact Euclid step (a >= b)
     const double qd = sv_words_to_double(a) / sv_words_to_double(b) * (1.0 - 0x1p-40);
     if (qd >= 4294967295.0) {  // (probability ~2^-32 per step) use (h, 1)
       bail = true;
