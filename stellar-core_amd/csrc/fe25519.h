@@ -137,18 +137,24 @@ SV_HD void fe_carry_wide(fe& out, uint64_t h[10]) {
 #define SV_MAD_PAIRS 4
 #endif
 // (k must fold to a constant: every caller is a fully unrolled loop)
+#define SV_MAD_I(L, H) \
+  asm("v_mad_u64_u32 %0, s[" #L ":" #H "], %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "s" #L, "s" #H)
+#define SV_MAD_A(L, H) \
+  asm("v_mad_u64_u32 %0, s[" #L ":" #H "], %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "s" #L, "s" #H)
+#define SV_MAD_SWITCH(M)      \
+  switch (k % SV_MAD_PAIRS) { \
+    case 0: M(94, 95); break; \
+    case 1: M(92, 93); break; \
+    case 2: M(90, 91); break; \
+    case 3: M(88, 89); break; \
+    case 4: M(86, 87); break; \
+    case 5: M(84, 85); break; \
+    case 6: M(82, 83); break; \
+    default: M(80, 81); break; \
+  }
 SV_HD void sv_mad_init_k(uint64_t& acc, uint32_t a, uint32_t b, int k) {
 #if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
-#if SV_MAD_PAIRS > 0
-  k %= SV_MAD_PAIRS;
-  if (k == 0) asm("v_mad_u64_u32 %0, s[94:95], %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "s94", "s95");
-  else if (k == 1) asm("v_mad_u64_u32 %0, s[92:93], %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "s92", "s93");
-  else if (k == 2) asm("v_mad_u64_u32 %0, s[90:91], %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "s90", "s91");
-  else asm("v_mad_u64_u32 %0, s[88:89], %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "s88", "s89");
-#else
-  (void)k;
-  asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b) : "vcc");
-#endif
+  SV_MAD_SWITCH(SV_MAD_I)
 #else
   (void)k;
   acc = (uint64_t)a * b;
@@ -156,16 +162,7 @@ SV_HD void sv_mad_init_k(uint64_t& acc, uint32_t a, uint32_t b, int k) {
 }
 SV_HD void sv_mad_k(uint64_t& acc, uint32_t a, uint32_t b, int k) {
 #if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
-#if SV_MAD_PAIRS > 0
-  k %= SV_MAD_PAIRS;
-  if (k == 0) asm("v_mad_u64_u32 %0, s[94:95], %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "s94", "s95");
-  else if (k == 1) asm("v_mad_u64_u32 %0, s[92:93], %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "s92", "s93");
-  else if (k == 2) asm("v_mad_u64_u32 %0, s[90:91], %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "s90", "s91");
-  else asm("v_mad_u64_u32 %0, s[88:89], %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "s88", "s89");
-#else
-  (void)k;
-  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
-#endif
+  SV_MAD_SWITCH(SV_MAD_A)
 #else
   (void)k;
   acc += (uint64_t)a * b;
@@ -246,6 +243,20 @@ SV_HD void fe_sq2(fe& h, const fe& f) {
   fe_carry_wide(h, c);
   SV_FENCE();
 }
+// Unfenced forms: the next field operation may be scheduled into this one
+// (pairs of independent operations overlap one's carry chain with the other's
+// products, at the cost of ~20 more live VGPRs).
+SV_HD void fe_mul_nf(fe& h, const fe& f, const fe& g) {
+  uint64_t c[10];
+  fe_mul_cols<false>(c, f, g);
+  fe_carry_wide(h, c);
+}
+SV_HD void fe_sq_nf(fe& h, const fe& f) {
+  uint64_t c[10];
+  fe_sq_cols<false>(c, f);
+  fe_carry_wide(h, c);
+}
+
 // n successive squarings (rolled loop: keeps the code object small)
 SV_HD void fe_sqn(fe& h, const fe& f, int n) {
   fe_sq(h, f);

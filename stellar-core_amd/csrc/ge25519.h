@@ -23,6 +23,14 @@
 
 #include "fe25519.h"
 
+// Overlap pairs of independent field operations in the hot formulas (A/B knobs)
+#ifndef SV_OVL_DBL
+#define SV_OVL_DBL 0
+#endif
+#ifndef SV_OVL_P1P1
+#define SV_OVL_P1P1 0
+#endif
+
 struct ge_p2 { fe X, Y, Z; };
 struct ge_p3 { fe X, Y, Z, T; };
 struct ge_p1p1 { fe X, Y, Z, T; };
@@ -43,9 +51,17 @@ SV_HD void ge_p2_identity(ge_p2& p) {
 SV_HD void ge_dbl(ge_p1p1& r, const fe& X, const fe& Y, const fe& Z) {
   fe XX, YY, ZZ2, A, AA;
   fe_add(A, X, Y);
+#if SV_OVL_DBL
+  fe_sq_nf(AA, A);
+#else
   fe_sq(AA, A);
+#endif
   fe_sq(XX, X);
+#if SV_OVL_DBL
+  fe_sq_nf(YY, Y);
+#else
   fe_sq(YY, Y);
+#endif
   fe_sq2(ZZ2, Z);
   fe_add(r.Y, YY, XX);    // y^2 + x^2            M2
   fe_sub(r.Z, YY, XX);    // y^2 - x^2            M3
@@ -72,7 +88,11 @@ SV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
 // matters: p.X (up to M5 after a doubling) is always the f operand.
 SV_HD void ge_p1p1_to_p3_opt(ge_p3& r, const ge_p1p1& p, bool wantT) {
   if (wantT) fe_mul(r.T, p.X, p.Y);
+#if SV_OVL_P1P1
+  fe_mul_nf(r.X, p.X, p.T);
+#else
   fe_mul(r.X, p.X, p.T);
+#endif
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
 }

@@ -27,6 +27,7 @@
 
 extern "C" {
 size_t sv_ws_bytes_per_block(void);
+size_t sv_ws_bytes(unsigned grid);
 size_t sv_btab_bytes(void);
 int sv_block_threads(void);
 hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s);
@@ -118,7 +119,7 @@ int init_device(Device& D, int id) {
   SV_HIP(sv_launch_btab_init((uint32_t*)D.btab, D.stream));
   const int per_cu = sv_occupancy_blocks_per_cu();
   D.grid = (unsigned)(D.cus * per_cu);
-  const size_t ws_bytes = (size_t)D.grid * sv_ws_bytes_per_block();
+  const size_t ws_bytes = sv_ws_bytes(D.grid);
   hipError_t e = hipMalloc(&D.ws, ws_bytes);
   if (e != hipSuccess) return fail(SV_ERR_ALLOC, std::string("workspace hipMalloc: ") + hipGetErrorString(e));
   SV_HIP(hipStreamSynchronize(D.stream));

@@ -224,6 +224,117 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_lat_ker
   }
 }
 
+// ---------------------------------------------- split form (SV_SPLIT = 1)
+// The per-signature phases (SHA-512, checks, decompression, mod L, Euclid,
+// tables, digits) and the scalar multiplication run as two kernels over a
+// chunk of up to SV_CHUNK signatures:
+//   sv_prep_kernel  one lane per signature, SV_PREP_WAVES waves/SIMD (the
+//                   phases are serial chains that need the extra waves to
+//                   hide their latency); writes the signature's tables and a
+//                   7-quad digit record into the chunk workspace, and each
+//                   wave's window count W into wmax[group].
+//   sv_main_kernel  the hot loop only, 2 waves/SIMD at 256 VGPRs, persistent.
+// Workspace per signature of the chunk: SV_SLOT_QUADS_L quads of tables, then
+// (separate array) SV_REC_QUADS quads of digits/flags.
+#ifndef SV_SPLIT
+#define SV_SPLIT 1
+#endif
+#ifndef SV_PREP_WAVES
+#define SV_PREP_WAVES 3
+#endif
+#ifndef SV_CHUNK
+#define SV_CHUNK (1u << 20)
+#endif
+#define SV_REC_QUADS 7
+// record flags (quad 6, .y)
+#define SV_REC_RNEG 1u
+#define SV_REC_TOP8A 2u
+#define SV_REC_TOP8R 4u
+#define SV_REC_OK 8u
+
+struct sv_cparams {
+  sv_kparams k;
+  uint64_t start;  // first signature of the chunk
+  uint64_t cnt;    // signatures in the chunk (<= SV_CHUNK)
+  sv_u4* rec;      // SV_CHUNK x SV_REC_QUADS
+  uint32_t* wmax;  // SV_CHUNK / 64
+};
+
+template <int MODE>
+__global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cparams c) {
+  const sv_kparams& p = c.k;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // index in the chunk
+  if (li - lane >= c.cnt) return;                                        // (wave-uniform)
+  const bool active = li < c.cnt;
+  const uint64_t ii = c.start + (active ? li : c.cnt - 1);  // idle tail lanes redo the last item
+  sv_u4* tabA = p.ws + li * SV_SLOT_QUADS_L;
+  sv_u4* tabR = tabA + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
+  uint32_t A[8], S[8], hram[16], R[8];
+  sv_load_and_hash<MODE>(p, ii, A, S, hram);
+  sv_unpack2(R, p.sig + 4 * ii);
+  sv_lat lat;
+  const bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR);
+  const int wl = sv_lat_windows(lat.bits);
+  int W = SV_LAT_MIN_WINDOWS;
+  while (__ballot(wl > W) != 0) ++W;
+  W = __builtin_amdgcn_readfirstlane(W);
+  sv_lat_digits D;
+  sv_lat_prepare(D, lat, S, W);
+  const uint32_t flags = (D.rneg ? SV_REC_RNEG : 0u) | (D.top8A ? SV_REC_TOP8A : 0u) |
+                         (D.top8R ? SV_REC_TOP8R : 0u) | (ok ? SV_REC_OK : 0u);
+  sv_u4* r = c.rec + li * SV_REC_QUADS;
+  r[0] = sv_u4{D.dA[0], D.dA[1], D.dA[2], D.dA[3]};
+  r[1] = sv_u4{D.dA[4], D.dA[5], D.dA[6], D.dA[7]};
+  r[2] = sv_u4{D.dR[0], D.dR[1], D.dR[2], D.dR[3]};
+  r[3] = sv_u4{D.dR[4], D.dR[5], D.dR[6], D.dR[7]};
+  r[4] = sv_u4{D.dB[0], D.dB[1], D.dB[2], D.dB[3]};
+  r[5] = sv_u4{D.dB[4], D.dB[5], D.dB[6], D.dB[7]};
+  r[6] = sv_u4{D.dB[8], flags, 0u, 0u};
+  if (lane == 0) c.wmax[li >> 6] = (uint32_t)W;
+}
+
+__global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_main_kernel(sv_cparams c) {
+  const sv_kparams& p = c.k;
+  __shared__ sv_u4 s_stage[SV_BLOCK / 64][2 * SV_LTAB_QUADS * 64];  // per-wave A and R entry stage
+  const uint32_t lane = threadIdx.x & 63u;
+  sv_u4* stage = s_stage[threadIdx.x >> 6];
+  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const sv_u4* btab0 = p.btab;
+  const sv_u4* btab1 = p.btab + SV_BTAB_ENTRIES * SV_BTAB_QUADS;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = gtid - lane; base < c.cnt; base += stride) {
+    const uint64_t li = base + lane;  // (slots exist up to the chunk's last full wave)
+    const bool active = li < c.cnt;
+    const sv_u4* tabA = p.ws + li * SV_SLOT_QUADS_L;
+    const sv_u4* tabR = tabA + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
+    const sv_u4* r = c.rec + li * SV_REC_QUADS;
+    sv_lat_digits D;
+    bool pre_ok;
+    {
+      const sv_u4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3], q4 = r[4], q5 = r[5], q6 = r[6];
+      D.dA[0] = q0.x; D.dA[1] = q0.y; D.dA[2] = q0.z; D.dA[3] = q0.w;
+      D.dA[4] = q1.x; D.dA[5] = q1.y; D.dA[6] = q1.z; D.dA[7] = q1.w;
+      D.dR[0] = q2.x; D.dR[1] = q2.y; D.dR[2] = q2.z; D.dR[3] = q2.w;
+      D.dR[4] = q3.x; D.dR[5] = q3.y; D.dR[6] = q3.z; D.dR[7] = q3.w;
+      D.dB[0] = q4.x; D.dB[1] = q4.y; D.dB[2] = q4.z; D.dB[3] = q4.w;
+      D.dB[4] = q5.x; D.dB[5] = q5.y; D.dB[6] = q5.z; D.dB[7] = q5.w;
+      D.dB[8] = q6.x;
+      D.rneg = (q6.y & SV_REC_RNEG) != 0;
+      D.top8A = (q6.y & SV_REC_TOP8A) != 0;
+      D.top8R = (q6.y & SV_REC_TOP8R) != 0;
+      pre_ok = (q6.y & SV_REC_OK) != 0;
+    }
+    const int W = (int)__builtin_amdgcn_readfirstlane(c.wmax[li >> 6]);
+    ge_p3 P;
+    sv_lat_scalarmult<true>(P, D, W, tabA, tabR, btab0, btab1, stage);
+    const bool ok = pre_ok && sv_is_identity(P) && active;
+    if (active) p.verdict[c.start + li] = ok ? 1 : 0;
+    const uint64_t mask = __ballot(ok);
+    if (p.bitmap != nullptr && lane == 0) p.bitmap[(c.start + base) >> 6] = mask;
+  }
+}
+
 __global__ void sv_btab_init_kernel(uint32_t* btab) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < SV_BTAB_ENTRIES) sv_btab_entry(btab + e * SV_BTAB_STRIDE, e);
@@ -286,6 +397,16 @@ int sv_debug_phase_cycles(unsigned long long out[8], int reset) {
 #endif
 
 size_t sv_ws_bytes_per_block(void) { return (size_t)SV_BLOCK * SV_SLOT_QUADS * sizeof(sv_u4); }
+// Whole device workspace: the persistent grid's per-lane slots (fused verify
+// kernel, signer) or, split, one chunk's tables + digit records + window counts.
+size_t sv_ws_bytes(unsigned grid) {
+  size_t b = (size_t)grid * sv_ws_bytes_per_block();
+#if SV_LATTICE && SV_SPLIT
+  const size_t s = (size_t)SV_CHUNK * (SV_SLOT_QUADS_L + SV_REC_QUADS) * sizeof(sv_u4) + (SV_CHUNK / 64) * 4;
+  if (s > b) b = s;
+#endif
+  return b;
+}
 size_t sv_btab_bytes(void) { return (size_t)SV_NBTAB * SV_BTAB_DWORDS * 4; }
 int sv_block_threads(void) { return SV_BLOCK; }
 
@@ -296,6 +417,14 @@ hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s) {
 
 int sv_occupancy_blocks_per_cu(void) {
   int b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+#if SV_LATTICE && SV_SPLIT
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, sv_main_kernel, SV_BLOCK, 0) != hipSuccess) b0 = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b3, sv_sign_kernel, SV_BLOCK, 0) != hipSuccess) b3 = 1;
+  const int ms = b0 > b3 ? b0 : b3;
+  (void)b1;
+  (void)b2;
+  return ms < 1 ? 1 : ms;
+#else
 #if SV_LATTICE
 #define SV_VK sv_verify_lat_kernel
 #else
@@ -310,6 +439,7 @@ int sv_occupancy_blocks_per_cu(void) {
   if (b2 > m) m = b2;
   if (b3 > m) m = b3;
   return m < 1 ? 1 : m;
+#endif
 }
 
 hipError_t sv_launch_verify(int mode, unsigned grid, const void* pk, const void* sig, const void* msg,
@@ -327,7 +457,26 @@ hipError_t sv_launch_verify(int mode, unsigned grid, const void* pk, const void*
   p.bitmap = (uint64_t*)bitmap;
   p.ws = (sv_u4*)ws;
   p.btab = (const sv_u4*)btab;
-#if SV_LATTICE
+#if SV_LATTICE && SV_SPLIT
+  sv_u4* rec = p.ws + (size_t)SV_CHUNK * SV_SLOT_QUADS_L;
+  uint32_t* wmax = (uint32_t*)(rec + (size_t)SV_CHUNK * SV_REC_QUADS);
+  for (uint64_t start = 0; start < n; start += SV_CHUNK) {
+    sv_cparams c;
+    c.k = p;
+    c.start = start;
+    c.cnt = n - start < SV_CHUNK ? n - start : SV_CHUNK;
+    c.rec = rec;
+    c.wmax = wmax;
+    const unsigned pg = (unsigned)((c.cnt + SV_BLOCK - 1) / SV_BLOCK);
+    if (mode == 0)
+      hipLaunchKernelGGL(sv_prep_kernel<0>, dim3(pg), dim3(SV_BLOCK), 0, s, c);
+    else if (mode == 1)
+      hipLaunchKernelGGL(sv_prep_kernel<1>, dim3(pg), dim3(SV_BLOCK), 0, s, c);
+    else
+      hipLaunchKernelGGL(sv_prep_kernel<2>, dim3(pg), dim3(SV_BLOCK), 0, s, c);
+    hipLaunchKernelGGL(sv_main_kernel, dim3(grid < pg ? grid : pg), dim3(SV_BLOCK), 0, s, c);
+  }
+#elif SV_LATTICE
   if (mode == 0)
     hipLaunchKernelGGL(sv_verify_lat_kernel<0>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
   else if (mode == 1)

@@ -2,7 +2,9 @@
 """Summarise a rocprofv3 profile directory of bench.py runs (developer tool).
 
 Reads <dir>/kt/*_kernel_stats.csv and every <dir>/*/*_counter_collection.csv,
-averages each counter over the sv_verify_kernel<0> dispatches and prints a
+averages each counter over the verify path's dispatches (split form: the
+sv_prep_kernel<0> + sv_main_kernel pair, summed per verify launch; fused form:
+sv_verify_lat_kernel<0>) and prints a
 JSON summary with per-launch HBM traffic (FETCH_SIZE doubled per
 MI355X_MICROARCH.md §HBM for 16-B streaming reads is NOT applied here: our
 reads are 16-B per-lane gathers, so both the raw and the doubled value are
@@ -25,28 +27,42 @@ def main():
     if "--batch" in sys.argv:
         batch = int(sys.argv[sys.argv.index("--batch") + 1])
     out = {"profile_dir": d, "batch": batch}
+    pat = re.compile(r"sv_verify(_lat)?_kernel<0>|sv_prep_kernel<0>|sv_main_kernel")
     ks = glob.glob(os.path.join(d, "kt", "*_kernel_stats.csv"))
     if ks:
+        per = {}
         for r in csv.DictReader(open(ks[0])):
-            if re.search(r"sv_verify(_lat)?_kernel<0>", r["Name"]):
-                out["kernel"] = r["Name"]
-                out["calls"] = int(r["Calls"])
-                out["avg_ns"] = float(r["AverageNs"])
-                out["min_ns"] = float(r["MinNs"])
-                out["max_ns"] = float(r["MaxNs"])
-    vals = defaultdict(list)
+            if pat.search(r["Name"]):
+                per[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                  "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
+        if per:
+            out["kernel"] = " + ".join(sorted(per))
+            out["kernels"] = per
+            out["calls"] = min(v["calls"] for v in per.values())
+            # one verify launch = one dispatch of each kernel of the path
+            for k in ("avg_ns", "min_ns", "max_ns"):
+                out[k] = sum(v[k] for v in per.values())
+    # per kernel: counter -> list over dispatches; a launch's value = sum over the path's kernels
+    vals = defaultdict(lambda: defaultdict(list))
     meta = {}
     for f in glob.glob(os.path.join(d, "*", "*_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if not re.search(r"sv_verify(_lat)?_kernel<0>", r["Kernel_Name"]):
+            if not pat.search(r["Kernel_Name"]):
                 continue
             if int(r["Grid_Size"]) < 1024:
                 continue
-            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
-                                      "Accum_VGPR_Count", "SGPR_Count")}
-    avg = {k: sum(v) / len(v) for k, v in vals.items()}
+            vals[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta[r["Kernel_Name"]] = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
+                                                        "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count")}
+    avg = defaultdict(float)
+    per_kernel = {}
+    for kn, cv in vals.items():
+        per_kernel[kn] = {c: sum(v) / len(v) for c, v in cv.items()}
+        for c, a in per_kernel[kn].items():
+            avg[c] += a
+    avg = dict(avg)
     out["dispatch"] = meta
+    out["counters_avg_per_launch_by_kernel"] = per_kernel
     out["counters_avg_per_launch"] = avg
     if "FETCH_SIZE" in avg:
         out["fetch_bytes_per_launch_raw"] = avg["FETCH_SIZE"] * 1024
