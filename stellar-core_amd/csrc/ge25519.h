@@ -151,8 +151,30 @@ SV_HD void ge_cached_identity(ge_cached& c) {
 // with bit 255, exactly as libsodium does (so x = 0 with bit 255 set passes
 // here; such encodings are on the small-order blacklist anyway).
 // Returns true on success.
+// Tail of the decompression once x = u v^3 (u v^7)^((p-5)/8) is known.
+SV_HD bool ge_frombytes_finish(ge_p3& h, const fe& u, const fe& v, const uint32_t w[8], bool negate) {
+  fe vxx, chk, chk2, xs, sq;
+  fe_sq(vxx, h.X);
+  fe_mul(vxx, vxx, v);
+  fe_sub(chk, vxx, u);
+  fe_add(chk2, vxx, u);
+  const bool m_ok = fe_iszero(chk);
+  const bool p_ok = fe_iszero(chk2);
+  fe_const_sqrtm1(sq);
+  fe_mul(xs, h.X, sq);
+  fe_cmov(h.X, xs, !m_ok);
+  const uint32_t sign = w[7] >> 31;
+  fe nx;
+  fe_neg(nx, h.X);
+  const bool flip = negate ? (fe_isnegative(h.X) == sign) : (fe_isnegative(h.X) != sign);
+  fe_cmov(h.X, nx, flip);
+  fe_weak(h.X);
+  fe_mul(h.T, h.X, h.Y);
+  return m_ok || p_ok;
+}
+
 SV_COLD bool ge_frombytes(ge_p3& h, const uint32_t w[8], bool negate) {
-  fe u, v, v3, vxx, chk, chk2, one, d, xs, sq;
+  fe u, v, v3, one, d;
   fe_1(one);
   fe_const_d(d);
   fe_frombytes(h.Y, w);
@@ -171,23 +193,40 @@ SV_COLD bool ge_frombytes(ge_p3& h, const uint32_t w[8], bool negate) {
   fe_pow22523(h.X, h.X);
   fe_mul(h.X, h.X, v3);
   fe_mul(h.X, h.X, u);  // u v^3 (u v^7)^((p-5)/8)
-  fe_sq(vxx, h.X);
-  fe_mul(vxx, vxx, v);
-  fe_sub(chk, vxx, u);
-  fe_add(chk2, vxx, u);
-  const bool m_ok = fe_iszero(chk);
-  const bool p_ok = fe_iszero(chk2);
-  fe_const_sqrtm1(sq);
-  fe_mul(xs, h.X, sq);
-  fe_cmov(h.X, xs, !m_ok);
-  const uint32_t sign = w[7] >> 31;
-  fe nx;
-  fe_neg(nx, h.X);
-  const bool flip = negate ? (fe_isnegative(h.X) == sign) : (fe_isnegative(h.X) != sign);
-  fe_cmov(h.X, nx, flip);
-  fe_weak(h.X);
-  fe_mul(h.T, h.X, h.Y);
-  return m_ok || p_ok;
+  return ge_frombytes_finish(h, u, v, w, negate);
+}
+
+// Two decompressions (-P1, -P2) with their exponentiation chains interleaved;
+// per point exactly ge_frombytes(.., negate = true).
+SV_COLD void ge_frombytes_neg_x2(ge_p3& h1, bool& ok1, const uint32_t w1[8], ge_p3& h2, bool& ok2,
+                                 const uint32_t w2[8]) {
+  fe u1, v1, c1, u2, v2, c2, one, d;
+  fe_1(one);
+  fe_const_d(d);
+  fe_frombytes(h1.Y, w1);
+  fe_frombytes(h2.Y, w2);
+  fe_1(h1.Z);
+  fe_1(h2.Z);
+  fe_sq_x2(u1, h1.Y, u2, h2.Y);
+  fe_mul_x2(v1, u1, d, v2, u2, d);
+  fe_sub(u1, u1, one);
+  fe_weak(u1);
+  fe_sub(u2, u2, one);
+  fe_weak(u2);
+  fe_add(v1, v1, one);
+  fe_weak(v1);
+  fe_add(v2, v2, one);
+  fe_weak(v2);
+  fe_sq_x2(c1, v1, c2, v2);
+  fe_mul_x2(c1, c1, v1, c2, c2, v2);  // v^3
+  fe_sq_x2(h1.X, c1, h2.X, c2);
+  fe_mul_x2(h1.X, h1.X, v1, h2.X, h2.X, v2);
+  fe_mul_x2(h1.X, h1.X, u1, h2.X, h2.X, u2);  // u v^7
+  fe_pow22523_x2(h1.X, h1.X, h2.X, h2.X);
+  fe_mul_x2(h1.X, h1.X, c1, h2.X, h2.X, c2);
+  fe_mul_x2(h1.X, h1.X, u1, h2.X, h2.X, u2);  // u v^3 (u v^7)^((p-5)/8)
+  ok1 = ge_frombytes_finish(h1, u1, v1, w1, true);
+  ok2 = ge_frombytes_finish(h2, u2, v2, w2, true);
 }
 
 // canonical encoding of a projective point given 1/Z (8 little-endian words)

@@ -31,7 +31,28 @@ SV_CONST uint64_t SV_SHA512_K[80] = {
     0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
     0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
 
-SV_HD uint64_t sv_rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate (n a compile-time constant, 0 < n < 64).  Device: two
+// v_alignbit_b32 on the 32-bit halves (LLVM otherwise expands it into two
+// 64-bit shifts and two ORs).
+SV_HD uint64_t sv_rotr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t rlo, rhi;
+  if (n < 32) {
+    rlo = __builtin_amdgcn_alignbit(hi, lo, n);
+    rhi = __builtin_amdgcn_alignbit(lo, hi, n);
+  } else if (n == 32) {
+    rlo = hi;
+    rhi = lo;
+  } else {
+    rlo = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+    rhi = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+  }
+  return ((uint64_t)rhi << 32) | rlo;
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
 SV_HD uint32_t sv_bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }
@@ -47,26 +68,30 @@ SV_HD void sha512_init(uint64_t st[8]) {
   st[6] = 0x1f83d9abfb41bd6bULL; st[7] = 0x5be0cd19137e2179ULL;
 }
 
-// One compression.  The 80 rounds run as 5 rolled passes of 16 unrolled
-// rounds, so the message schedule stays in registers with static indices and
-// the round constants are scalar (uniform) loads.
-SV_COLD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
+// One compression, inlined into its caller so the state and the message
+// schedule live in registers (as an out-of-line function with array
+// arguments the schedule went through memory every round).  Rounds 0-15 run
+// unrolled without the schedule update; rounds 16-79 as 4 rolled passes of 16
+// unrolled rounds (static register indices, uniform round-constant loads).
+#define SV_SHA512_ROUND(Wi, Ki)                                                       \
+  do {                                                                               \
+    const uint64_t S1 = sv_rotr64(e, 14) ^ sv_rotr64(e, 18) ^ sv_rotr64(e, 41);       \
+    const uint64_t ch = (e & f) ^ (~e & g);                                           \
+    const uint64_t t1 = h + S1 + ch + (Ki) + (Wi);                                    \
+    const uint64_t S0 = sv_rotr64(a, 28) ^ sv_rotr64(a, 34) ^ sv_rotr64(a, 39);       \
+    const uint64_t mj = (a & b) ^ (c & (a ^ b));                                      \
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;           \
+  } while (0)
+SV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-  SV_NOUNROLL for (int pass = 0; pass < 5; ++pass) {
+  SV_UNROLL for (int i = 0; i < 16; ++i) SV_SHA512_ROUND(w[i], SV_SHA512_K[i]);
+  SV_NOUNROLL for (int pass = 1; pass < 5; ++pass) {
     SV_UNROLL for (int i = 0; i < 16; ++i) {
-      if (pass > 0) {
-        const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-        const uint64_t s0 = sv_rotr64(w15, 1) ^ sv_rotr64(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = sv_rotr64(w2, 19) ^ sv_rotr64(w2, 61) ^ (w2 >> 6);
-        w[i] = w[i] + s0 + w[(i + 9) & 15] + s1;
-      }
-      const uint64_t S1 = sv_rotr64(e, 14) ^ sv_rotr64(e, 18) ^ sv_rotr64(e, 41);
-      const uint64_t ch = (e & f) ^ (~e & g);
-      const uint64_t t1 = h + S1 + ch + SV_SHA512_K[16 * pass + i] + w[i];
-      const uint64_t S0 = sv_rotr64(a, 28) ^ sv_rotr64(a, 34) ^ sv_rotr64(a, 39);
-      const uint64_t mj = (a & b) ^ (c & (a ^ b));
-      const uint64_t t2 = S0 + mj;
-      h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+      const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+      const uint64_t s0 = sv_rotr64(w15, 1) ^ sv_rotr64(w15, 8) ^ (w15 >> 7);
+      const uint64_t s1 = sv_rotr64(w2, 19) ^ sv_rotr64(w2, 61) ^ (w2 >> 6);
+      w[i] = w[i] + s0 + w[(i + 9) & 15] + s1;
+      SV_SHA512_ROUND(w[i], SV_SHA512_K[16 * pass + i]);
     }
   }
   st[0] += a; st[1] += b; st[2] += c; st[3] += d;

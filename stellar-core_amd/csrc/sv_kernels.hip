@@ -240,7 +240,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_lat_ker
 #define SV_SPLIT 1
 #endif
 #ifndef SV_PREP_WAVES
-#define SV_PREP_WAVES 3
+#define SV_PREP_WAVES 2
 #endif
 #ifndef SV_CHUNK
 #define SV_CHUNK (1u << 20)
@@ -270,11 +270,46 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   const uint64_t ii = c.start + (active ? li : c.cnt - 1);  // idle tail lanes redo the last item
   sv_u4* tabA = p.ws + li * SV_SLOT_QUADS_L;
   sv_u4* tabR = tabA + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
+#ifdef SV_PHASE_PROF
+  unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+#endif
   uint32_t A[8], S[8], hram[16], R[8];
+#ifdef SV_PHASE_PROF
+  {
+    uint32_t M[8];
+    sv_unpack2(A, p.pk + 2 * ii);
+    sv_unpack2(R, p.sig + 4 * ii);
+    sv_unpack2(S, p.sig + 4 * ii + 2);
+    sv_unpack2(M, (const sv_u4*)(p.msg) + 2 * ii);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    SV_PHASE(5);
+    sha512_ram32(hram, R, A, M);
+  }
+#else
   sv_load_and_hash<MODE>(p, ii, A, S, hram);
   sv_unpack2(R, p.sig + 4 * ii);
+#endif
+  SV_PHASE(0);
   sv_lat lat;
+#ifdef SV_PHASE_PROF
+  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
+            sv_point_canonical(R);
+  ge_p3 negA, negR;
+  ok = ge_frombytes(negA, A, true) && ok;
+  ok = ge_frombytes(negR, R, true) && ok;
+  SV_PHASE(1);
+  {
+    uint32_t h[8];
+    sc_reduce512(h, hram);
+    sc_lattice_reduce(lat, h);
+  }
+  SV_PHASE(2);
+  sv_build_ltab(tabA, negA);
+  sv_build_ltab(tabR, negR);
+  SV_PHASE(3);
+#else
   const bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR);
+#endif
   const int wl = sv_lat_windows(lat.bits);
   int W = SV_LAT_MIN_WINDOWS;
   while (__ballot(wl > W) != 0) ++W;
@@ -292,6 +327,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   r[5] = sv_u4{D.dB[4], D.dB[5], D.dB[6], D.dB[7]};
   r[6] = sv_u4{D.dB[8], flags, 0u, 0u};
   if (lane == 0) c.wmax[li >> 6] = (uint32_t)W;
+  SV_PHASE(4);
 }
 
 __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_main_kernel(sv_cparams c) {

@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """Developer tool: per-phase s_memtime breakdown of the verify kernel, from a
 variant built with -DSV_PHASE_PROF (tools/build_variants.sh prof "-DSV_PHASE_PROF").
-Usage: python tools/phase_prof.py variants/libsv_prof.so"""
+Usage: python tools/phase_prof.py variants/libsv_prof.so
+(split build: phases 0-4 are the prep kernel's; the main kernel is not instrumented)"""
 import ctypes
 import sys
 
 import torch  # noqa: F401  (load torch's HIP runtime first)
 
-NAMES = ["load+sha512", "checks+decode A,R", "mod L + Euclid", "tables A,R", "W + digits", "scalar mult",
+NAMES = ["sha512 (prep: after loads)", "checks+decode A,R", "mod L + Euclid", "tables A,R", "W + digits (+ record)", "scalar mult (prep: input loads)",
          "identity check", "-"]
 lib = ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_LOCAL)
 assert lib.sv_init() == 0
@@ -32,6 +33,6 @@ for it in range(3):
     lib.sv_debug_phase_cycles(cyc, 0)
 assert int(out.sum().item()) == n
 tot = sum(cyc)
-for i in range(7):
+for i in range(8):
     print("%-20s %6.2f %%  (%.0f per-wave cycles per signature group)" % (NAMES[i], 100.0 * cyc[i] / tot,
                                                                           cyc[i] / (n / 64)))
