@@ -123,34 +123,51 @@ SV_HD void sha512_ram32(uint32_t out[16], const uint32_t R[8], const uint32_t A[
   sha512_digest_le(out, st);
 }
 
-// SHA-512(R || A || M) for an arbitrary-length M read byte-wise from memory.
-// Stream byte k: k < 32 -> R, k < 64 -> A, k < 64+mlen -> M[k-64], then the
-// 0x80 pad, zeros, and the 128-bit big-endian bit length.
-SV_HD uint32_t sv_stream_byte(const uint32_t R[8], const uint32_t A[8], const uint8_t* m, uint32_t mlen,
-                              uint64_t k, uint64_t total_blocks) {
-  if (k < 32) return (R[k >> 2] >> (8 * (k & 3))) & 0xff;
-  if (k < 64) return (A[(k - 32) >> 2] >> (8 * (k & 3))) & 0xff;
-  const uint64_t mi = k - 64;
-  if (mi < mlen) return m[mi];
-  if (mi == mlen) return 0x80;
-  const uint64_t end = total_blocks * 128;
-  if (k >= end - 8) {
-    const uint64_t bits = (64 + (uint64_t)mlen) * 8;
-    return (uint32_t)(bits >> (8 * (end - 1 - k))) & 0xff;
+// Message bytes m[mi, mi + 8) as a big-endian SHA-512 word, bytes at or past
+// mlen replaced by the padding (0x80 at mlen, zeros after).  Reads aligned
+// dwords only, and only those holding at least one message byte (so never
+// past the message's last dword), then funnel-shifts them into place.
+SV_HD uint64_t sv_msg_word(const uint8_t* m, uint32_t mlen, uint32_t mi) {
+  const uintptr_t a = (uintptr_t)(m + mi), end = (uintptr_t)(m + mlen);
+  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3) * 8;
+  const uint32_t d0 = (uintptr_t)q < end ? q[0] : 0u;
+  const uint32_t d1 = (uintptr_t)(q + 1) < end ? q[1] : 0u;
+  const uint32_t d2 = (uintptr_t)(q + 2) < end ? q[2] : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh);
+  const uint32_t hi = __builtin_amdgcn_alignbit(d2, d1, sh);
+#else
+  const uint32_t lo = sh ? (d0 >> sh) | (d1 << (32 - sh)) : d0;
+  const uint32_t hi = sh ? (d1 >> sh) | (d2 << (32 - sh)) : d1;
+#endif
+  uint64_t v = ((uint64_t)hi << 32) | lo;  // byte j of the word at bits 8j
+  if (mlen < mi + 8) {
+    const uint32_t valid = mlen > mi ? mlen - mi : 0u;  // < 8
+    v &= (1ull << (8 * valid)) - 1;
+    if (mlen >= mi) v |= 0x80ull << (8 * (mlen - mi));
   }
-  return 0;
+  return sv_be64((uint32_t)v, (uint32_t)(v >> 32));
 }
 
+// SHA-512(R || A || M) for an arbitrary-length M in memory (any alignment).
+// Stream: R (32 B) || A (32 B) fill words 0-7 of block 0; message byte j is at
+// stream offset 64 + j, so every other word is 8 consecutive message bytes
+// (sv_msg_word); word 15 of the last block is the bit length (< 2^64).
 SV_HD void sha512_ram_var(uint32_t out[16], const uint32_t R[8], const uint32_t A[8], const uint8_t* m,
                           uint32_t mlen) {
   uint64_t st[8], w[16];
   sha512_init(st);
-  const uint64_t nblocks = (64 + (uint64_t)mlen + 16 + 1 + 127) / 128;
-  SV_NOUNROLL for (uint64_t blk = 0; blk < nblocks; ++blk) {
+  const uint32_t nblocks = (64u + mlen + 16u + 1u + 127u) / 128u;
+  SV_NOUNROLL for (uint32_t blk = 0; blk < nblocks; ++blk) {
     SV_UNROLL for (int t = 0; t < 16; ++t) {
-      uint64_t v = 0;
-      SV_NOUNROLL for (int j = 0; j < 8; ++j)
-        v = (v << 8) | sv_stream_byte(R, A, m, mlen, blk * 128 + 8 * t + j, nblocks);
+      uint64_t v;
+      if (t < 8 && blk == 0) {
+        v = t < 4 ? sv_be64(R[2 * t], R[2 * t + 1]) : sv_be64(A[2 * t - 8], A[2 * t - 7]);
+      } else {
+        v = sv_msg_word(m, mlen, 128u * blk + 8u * (uint32_t)t - 64u);
+      }
+      if (t == 15 && blk == nblocks - 1) v = (uint64_t)(64u + mlen) * 8u;
       w[t] = v;
     }
     sha512_compress(st, w);

@@ -119,6 +119,14 @@ def test_sha512_ram_paths(hostcore):
         m = rnd.bytes(n)
         hostcore.hc_sha512_ram(out, R, A, m, n, 0)
         assert out.raw == hashlib.sha512(R + A + m).digest(), n
+    # message at every alignment inside a larger buffer (the device reads
+    # aligned dwords and funnel-shifts them)
+    for n in (0, 1, 7, 8, 9, 47, 48, 49, 63, 64, 65, 200):
+        for off in range(4):
+            R, A = rnd.bytes(32), rnd.bytes(32)
+            buf = ctypes.create_string_buffer(rnd.bytes(off + n + 8), off + n + 8)
+            hostcore.hc_sha512_ram(out, R, A, ctypes.byref(buf, off), n, 0)
+            assert out.raw == hashlib.sha512(R + A + buf.raw[off:off + n]).digest(), (n, off)
     R, A, m = rnd.bytes(32), rnd.bytes(32), rnd.bytes(32)
     hostcore.hc_sha512_ram(out, R, A, m, 32, 1)
     assert out.raw == hashlib.sha512(R + A + m).digest()
