@@ -52,8 +52,25 @@ typedef struct sv_opts {
   uint32_t struct_size; /* sizeof(sv_opts), for forward compatibility */
   int32_t device;       /* -1 (default): shard contiguous slices over all devices; k >= 0: device k only */
   uint32_t max_devices; /* 0 (default): no limit; else use at most this many devices when device == -1 */
-  uint32_t flags;       /* reserved, must be 0 */
+  uint32_t flags;       /* 0 or one SV_FLAG_PATH_* (kernel path for this call); other bits must be 0 */
 } sv_opts;
+
+/* Kernel paths.  THROUGHPUT: one lane per signature, prep + main kernels per
+ * 2^20-signature chunk (large batches).  LATENCY: one quad of lanes per
+ * signature, every point operation split four ways (small, latency-bound
+ * batches such as SCP envelope floods).  AUTO picks LATENCY for batches of at
+ * most 12288 signatures (the sizes it runs in one pass over the GPU).
+ * Verdicts are identical on every path. */
+#define SV_PATH_AUTO 0
+#define SV_PATH_THROUGHPUT 1
+#define SV_PATH_LATENCY 2
+#define SV_FLAG_PATH_THROUGHPUT 0x1u
+#define SV_FLAG_PATH_LATENCY 0x2u
+#define SV_FLAG_PATH_MASK 0x3u
+
+/* Process-wide default path for calls that do not request one (the device
+ * API never does).  Returns the previous default, or SV_ERR_INVALID_ARG. */
+int sv_set_kernel_path(int path);
 
 /* Initialise every visible device (B-table, workspace, streams).  Idempotent.
  * Called implicitly by the verify entry points. */

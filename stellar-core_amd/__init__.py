@@ -26,7 +26,10 @@ LIB_PATH = os.path.join(_HERE, "libstellar_sigverify.so")
 
 
 VERIFY_KERNEL_SOURCES = ("sv_common.h", "fe25519.h", "ge25519.h", "sc25519.h", "lattice.h", "sha512_dev.h", "verify_core.h",
-                         "sv_kernels.hip")
+                         "quad.h", "sv_kernels.hip")
+
+# kernel paths (include/stellar_sigverify.h)
+PATH_AUTO, PATH_THROUGHPUT, PATH_LATENCY = 0, 1, 2
 
 
 def kernel_source_digest() -> str:
@@ -58,7 +61,7 @@ EXPORTED_SYMBOLS = (
     "sv_ed25519_verify_batch", "sv_ed25519_verify_batch_fixed", "sv_ed25519_verify_device",
     "sv_ed25519_sign_device", "sv_timing_enable", "sv_kernel_time", "sv_kernel_time_reset",
     "sv_device_synchronize", "sv_verify_cache_keys", "sv_ed25519_verify_batch_keyed", "sv_sha256_batch",
-    "sv_verify_cache_keys_device", "sv_sha256_device",
+    "sv_verify_cache_keys_device", "sv_sha256_device", "sv_set_kernel_path",
 )
 
 
@@ -264,6 +267,17 @@ def verify_device(device: int, d_pk: int, d_sig: int, d_msg: int, n: int, d_verd
 def sign_device(device: int, d_seed: int, d_msg32: int, n: int, d_pk: int, d_sig: int, stream: int = 0) -> None:
     lib = load_library()
     _check(lib.sv_ed25519_sign_device(device, d_seed, d_msg32, n, d_pk, d_sig, stream or None))
+
+
+def set_kernel_path(path: int) -> int:
+    """Process-wide default kernel path (PATH_AUTO / PATH_THROUGHPUT /
+    PATH_LATENCY) for calls that do not request one; returns the previous."""
+    lib = load_library()
+    lib.sv_set_kernel_path.argtypes = [ctypes.c_int]
+    rc = lib.sv_set_kernel_path(int(path))
+    if rc < 0:
+        _check(rc)
+    return rc
 
 
 def timing_enable(on: bool = True) -> None:

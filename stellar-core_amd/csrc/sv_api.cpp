@@ -32,7 +32,7 @@ size_t sv_btab_bytes(void);
 int sv_block_threads(void);
 hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s);
 int sv_occupancy_blocks_per_cu(void);
-hipError_t sv_launch_verify(int mode, unsigned grid, const void* pk, const void* sig, const void* msg,
+hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, const void* sig, const void* msg,
                             const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n,
                             void* verdict, void* bitmap, void* ws, const void* btab, hipStream_t s);
 hipError_t sv_launch_sign(unsigned grid, const void* seed, const void* msg, uint64_t n, void* pk, void* sig,
@@ -105,6 +105,24 @@ std::mutex g_mu;
 std::vector<Device*> g_devs;
 bool g_inited = false;
 std::atomic<int> g_timing{0};
+std::atomic<int> g_path{SV_PATH_AUTO};  // sv_set_kernel_path
+
+// Batches up to this size take the latency kernel under SV_PATH_AUTO
+// (measured crossover on MI355X).
+constexpr uint64_t kQuickMax = 12288;
+
+// Kernel path for one launch: an explicit per-call request (sv_opts.flags),
+// else the process default, else by batch size.
+int resolve_path(int requested, uint64_t n) {
+  int p = requested != SV_PATH_AUTO ? requested : g_path.load();
+  if (p == SV_PATH_AUTO) p = n <= kQuickMax ? SV_PATH_LATENCY : SV_PATH_THROUGHPUT;
+  return p;
+}
+int path_from_flags(uint32_t flags) {
+  if (flags & SV_FLAG_PATH_LATENCY) return SV_PATH_LATENCY;
+  if (flags & SV_FLAG_PATH_THROUGHPUT) return SV_PATH_THROUGHPUT;
+  return SV_PATH_AUTO;
+}
 
 int init_device(Device& D, int id) {
   D.id = id;
@@ -157,7 +175,7 @@ unsigned grid_for(const Device& D, uint64_t n) {
 }
 
 // Launch on D.stream (caller holds D.mu and has set the device).
-int launch_locked(Device& D, int mode, const void* pk, const void* sig, const void* msg, const uint64_t* off,
+int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig, const void* msg, const uint64_t* off,
                   const uint32_t* len, uint32_t fixed_len, uint64_t n, void* verdict, void* bitmap) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool timing = g_timing.load() != 0;
@@ -166,8 +184,8 @@ int launch_locked(Device& D, int mode, const void* pk, const void* sig, const vo
     SV_HIP(hipEventCreate(&e1));
     SV_HIP(hipEventRecord(e0, D.stream));
   }
-  SV_HIP(sv_launch_verify(mode, grid_for(D, n), pk, sig, msg, off, len, fixed_len, n, verdict, bitmap, D.ws,
-                          D.btab, D.stream));
+  SV_HIP(sv_launch_verify(mode, resolve_path(path, n), grid_for(D, n), pk, sig, msg, off, len, fixed_len, n, verdict,
+                          bitmap, D.ws, D.btab, D.stream));
   if (timing) {
     SV_HIP(hipEventRecord(e1, D.stream));
     D.pending.emplace_back(e0, e1);
@@ -196,7 +214,7 @@ int harvest_timing_locked(Device& D) {
 // (verdict != null) and/or the cache-key kernel (keys != null) on the same
 // stream, copy results back, sync.
 int host_slice(Device& D, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
-               const uint32_t* msg_len, uint32_t fixed_len, size_t n, uint8_t* verdict, uint8_t* keys) {
+               const uint32_t* msg_len, uint32_t fixed_len, size_t n, uint8_t* verdict, uint8_t* keys, int path) {
   std::lock_guard<std::mutex> g(D.mu);
   SV_HIP(hipSetDevice(D.id));
   int rc;
@@ -238,7 +256,7 @@ int host_slice(Device& D, const uint8_t* pk, const uint8_t* sig, const uint8_t* 
     SV_HIP(hipMemcpyAsync(keys, D.keys.p, n * 32, hipMemcpyDeviceToHost, D.stream));
   }
   if (verdict) {
-    if ((rc = launch_locked(D, mode, D.pk.p, D.sig.p, D.msg.p, (const uint64_t*)D.off.p,
+    if ((rc = launch_locked(D, mode, path, D.pk.p, D.sig.p, D.msg.p, (const uint64_t*)D.off.p,
                             (const uint32_t*)D.len.p, fixed_len, n, D.verdict.p, nullptr)))
       return rc;
     SV_HIP(hipMemcpyAsync(verdict, D.verdict.p, n, hipMemcpyDeviceToHost, D.stream));
@@ -287,7 +305,9 @@ int select_devices(const sv_opts* opts, std::vector<Device*>& out) {
   int dev = -1;
   uint32_t maxd = 0;
   if (opts) {
-    if (opts->struct_size < sizeof(sv_opts) || opts->flags != 0) return fail(SV_ERR_INVALID_ARG, "bad sv_opts");
+    if (opts->struct_size < sizeof(sv_opts) || (opts->flags & ~SV_FLAG_PATH_MASK) != 0 ||
+        (opts->flags & SV_FLAG_PATH_MASK) == SV_FLAG_PATH_MASK)
+      return fail(SV_ERR_INVALID_ARG, "bad sv_opts");
     dev = opts->device;
     maxd = opts->max_devices;
   }
@@ -351,7 +371,8 @@ int verify_host(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
   return shard(devs, n, [&](Device& D, size_t lo, size_t hi) {
     return host_slice(D, pk + 32 * lo, sig + 64 * lo, fixed_len ? msg + lo * (size_t)fixed_len : msg,
                       fixed_len ? nullptr : msg_off + lo, fixed_len ? nullptr : msg_len + lo, fixed_len, hi - lo,
-                      verdict ? verdict + lo : nullptr, keys ? keys + 32 * lo : nullptr);
+                      verdict ? verdict + lo : nullptr, keys ? keys + 32 * lo : nullptr,
+                      path_from_flags(opts ? opts->flags : 0u));
   });
 }
 
@@ -503,12 +524,17 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
   hipStream_t user = (hipStream_t)stream;
   SV_HIP(hipEventRecord(D.dep_in, user));
   SV_HIP(hipStreamWaitEvent(D.stream, D.dep_in, 0));
-  if ((rc = launch_locked(D, mode, d_pk, d_sig, d_msg, d_msg_off, d_msg_len, fixed_msg_len, n, d_verdict,
-                          d_bitmap)))
+  if ((rc = launch_locked(D, mode, SV_PATH_AUTO, d_pk, d_sig, d_msg, d_msg_off, d_msg_len, fixed_msg_len, n,
+                          d_verdict, d_bitmap)))
     return rc;
   SV_HIP(hipEventRecord(D.dep_out, D.stream));
   SV_HIP(hipStreamWaitEvent(user, D.dep_out, 0));
   return SV_OK;
+}
+
+int sv_set_kernel_path(int path) {
+  if (path != SV_PATH_AUTO && path != SV_PATH_THROUGHPUT && path != SV_PATH_LATENCY) return SV_ERR_INVALID_ARG;
+  return g_path.exchange(path);
 }
 
 int sv_ed25519_sign_device(int device, const void* d_seed, const void* d_msg32, size_t n, void* d_pk, void* d_sig,

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include "verify_core.h"
+#include "quad.h"
 
 #define SV_BLOCK 256
 #ifndef SV_STAGE_A
@@ -371,6 +372,137 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_main_kernel(sv
   }
 }
 
+// ------------------------------------------- latency path (quad.h)
+// One signature per quad of lanes, 16 signatures per single-wave workgroup.
+// Per quad: every lane hashes and reduces (redundantly, so all four hold the
+// digits); lanes of even role decompress A, odd roles R; roles 0 / 1 build
+// table_A / table_R into the workgroup's LDS; then the windowed scalar
+// multiplication runs with every point operation split over the quad.
+// Verdict bytes by role-0 lanes; the bitmap as one 16-bit store per workgroup
+// (bits 16 k .. 16 k + 15 of word k / 4).
+#define SV_QSIGS 16
+#define SV_QENT_DW 40  // cached entry: YpX, YmX, Z, T2d x 10 dwords
+
+// this lane's operand of cached entry e (LDS): role 0 T2d, role 1 Z, roles
+// 2 / 3 the (Y+X, Y-X) pair swapped when neg
+__device__ __forceinline__ void qd_load_cached(fe& o, const uint32_t* ent, uint32_t role, bool neg) {
+  const uint32_t comp = role == 0 ? 3u : role == 1 ? 2u : ((role == 2) != neg ? 0u : 1u);
+  const uint32_t* src = ent + 10 * comp;
+  SV_UNROLL for (int k = 0; k < 10; ++k) o.v[k] = src[k];
+}
+// this lane's operand of affine base-point entry e (global): role 0 2dxy,
+// role 1 the constant 1 (Z), roles 2 / 3 the (y+x, y-x) pair swapped when neg
+__device__ __forceinline__ void qd_load_affine(fe& o, const sv_u4* ent, uint32_t role, bool neg) {
+  const uint32_t comp = role == 0 ? 2u : ((role == 2) != neg ? 0u : 1u);
+  const sv_u4* src = ent + 3 * comp;
+  const sv_u4 a = src[0], b = src[1], c = src[2];
+  o.v[0] = a.x; o.v[1] = a.y; o.v[2] = a.z; o.v[3] = a.w;
+  o.v[4] = b.x; o.v[5] = b.y; o.v[6] = b.z; o.v[7] = b.w;
+  o.v[8] = c.x; o.v[9] = c.y;
+  if (role == 1) fe_1(o);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
+  __shared__ uint32_t s_tab[SV_QSIGS][2][SV_ATAB_ENTRIES][SV_QENT_DW];  // 46 KB
+  const uint32_t lane = threadIdx.x;
+  const uint32_t role = lane & 3u, sl = lane >> 2;
+  const qd_role q{role == 1, role == 2, role == 3};
+  const uint64_t i = (uint64_t)blockIdx.x * SV_QSIGS + sl;
+  const bool active = i < p.n;
+  const uint64_t ii = active ? i : p.n - 1;  // idle tail quads redo the last item
+  uint32_t A[8], S[8], hram[16], R[8];
+  sv_load_and_hash<MODE>(p, ii, A, S, hram);
+  sv_unpack2(R, p.sig + 4 * ii);
+  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
+            sv_point_canonical(R);
+  {
+    // decompress: even roles -A, odd roles -R; roles 0 / 1 keep their table
+    uint32_t E[8];
+    SV_UNROLL for (int k = 0; k < 8; ++k) E[k] = (role & 1u) ? R[k] : A[k];
+    ge_p3 Pt;
+    const uint32_t dok = ge_frombytes(Pt, E, true) ? 1u : 0u;
+    ok = ok && (qd_from<0>(dok) & qd_from<1>(dok)) != 0;
+    ge_cached c1, ce;
+    ge_p3_to_cached(c1, Pt);
+    ge_cached_identity(ce);
+    uint32_t* tab = &s_tab[sl][role & 1u][0][0];
+    const bool store = role < 2;
+    if (store) sv_store_lentry((sv_u4*)tab, ce);
+    if (store) sv_store_lentry((sv_u4*)(tab + SV_QENT_DW), c1);
+    ge_p3 P3 = Pt;
+    ge_p1p1 Qa;
+    SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
+      ge_add_preswapped(Qa, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, false);
+      ge_p1p1_to_p3(P3, Qa);
+      ge_p3_to_cached(ce, P3);
+      if (store) sv_store_lentry((sv_u4*)(tab + e * SV_QENT_DW), ce);
+    }
+  }
+  sv_lat lat;
+  {
+    uint32_t h[8];
+    sc_reduce512(h, hram);
+    sc_lattice_reduce(lat, h);
+  }
+  const int wl = sv_lat_windows(lat.bits);
+  int W = SV_LAT_MIN_WINDOWS;
+  while (__ballot(wl > W) != 0) ++W;
+  W = __builtin_amdgcn_readfirstlane(W);
+  sv_lat_digits D;
+  sv_lat_prepare(D, lat, S, W);
+  __syncthreads();  // tables visible to the whole quad
+
+  const sv_u4* btab0 = p.btab;
+  const sv_u4* btab1 = p.btab + SV_BTAB_ENTRIES * SV_BTAB_QUADS;
+  const uint32_t* tabA = &s_tab[sl][0][0][0];
+  const uint32_t* tabR = &s_tab[sl][1][0][0];
+  ge_p3 P;
+  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
+  SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
+    int32_t dA = sc_pop_top(D.dA, 4);
+    int32_t dR = sc_pop_top(D.dR, 4);
+    if (w == W - 1) {
+      if (D.top8A) dA = 8;
+      if (D.top8R) dR = 8;
+    }
+    if (D.rneg) dR = -dR;
+    const bool bwin = (w & 3) == 0 && (w >> 2) <= 8;
+    int32_t dB0 = 0, dB1 = 0;
+    fe b0, b1;
+    if (bwin) {
+      const uint32_t t = D.dB[8];
+      dB0 = ((int32_t)(t << 16)) >> 16;
+      dB1 = ((int32_t)t) >> 16;
+      SV_UNROLL for (int k = 8; k > 0; --k) D.dB[k] = D.dB[k - 1];
+      D.dB[0] = 0;
+      // issued before the doublings: the loads land while they run
+      qd_load_affine(b0, btab0 + (dB0 < 0 ? -dB0 : dB0) * SV_BTAB_QUADS, role, dB0 < 0);
+      qd_load_affine(b1, btab1 + (dB1 < 0 ? -dB1 : dB1) * SV_BTAB_QUADS, role, dB1 < 0);
+    }
+    if (w != W - 1) {
+      SV_NOUNROLL for (int k = 0; k < 4; ++k) qd_dbl(P, q, k == 3);
+    }
+    fe m;
+    qd_load_cached(m, tabA + (dA < 0 ? -dA : dA) * SV_QENT_DW, role, dA < 0);
+    qd_add(P, m, q, dA < 0, true);
+    qd_load_cached(m, tabR + (dR < 0 ? -dR : dR) * SV_QENT_DW, role, dR < 0);
+    qd_add(P, m, q, dR < 0, bwin);
+    if (bwin) {
+      qd_add(P, b0, q, dB0 < 0, true);
+      qd_add(P, b1, q, dB1 < 0, false);
+    }
+  }
+  ok = ok && sv_is_identity(P);
+  if (active && role == 0) p.verdict[i] = ok ? 1 : 0;
+  const uint64_t bal = __ballot(ok && active && role == 0);
+  if (p.bitmap != nullptr && lane == 0) {
+    uint16_t m16 = 0;
+    SV_UNROLL for (int k = 0; k < SV_QSIGS; ++k) m16 |= (uint16_t)(((bal >> (4 * k)) & 1u) << k);
+    ((uint16_t*)p.bitmap)[blockIdx.x] = m16;
+  }
+}
+
 __global__ void sv_btab_init_kernel(uint32_t* btab) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < SV_BTAB_ENTRIES) sv_btab_entry(btab + e * SV_BTAB_STRIDE, e);
@@ -478,7 +610,7 @@ int sv_occupancy_blocks_per_cu(void) {
 #endif
 }
 
-hipError_t sv_launch_verify(int mode, unsigned grid, const void* pk, const void* sig, const void* msg,
+hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, const void* sig, const void* msg,
                             const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n,
                             void* verdict, void* bitmap, void* ws, const void* btab, hipStream_t s) {
   sv_kparams p;
@@ -493,6 +625,19 @@ hipError_t sv_launch_verify(int mode, unsigned grid, const void* pk, const void*
   p.bitmap = (uint64_t*)bitmap;
   p.ws = (sv_u4*)ws;
   p.btab = (const sv_u4*)btab;
+#if SV_LATTICE
+  if (path == 2) {  // SV_PATH_LATENCY
+    const unsigned qg = (unsigned)((n + SV_QSIGS - 1) / SV_QSIGS);
+    if (mode == 0)
+      hipLaunchKernelGGL(sv_quick_kernel<0>, dim3(qg), dim3(64), 0, s, p);
+    else if (mode == 1)
+      hipLaunchKernelGGL(sv_quick_kernel<1>, dim3(qg), dim3(64), 0, s, p);
+    else
+      hipLaunchKernelGGL(sv_quick_kernel<2>, dim3(qg), dim3(64), 0, s, p);
+    return hipGetLastError();
+  }
+#endif
+  (void)path;
 #if SV_LATTICE && SV_SPLIT
   sv_u4* rec = p.ws + (size_t)SV_CHUNK * SV_SLOT_QUADS_L;
   uint32_t* wmax = (uint32_t*)(rec + (size_t)SV_CHUNK * SV_REC_QUADS);

@@ -34,6 +34,17 @@ def dev(sv):
     return torch.device("cuda", 0)
 
 
+@pytest.fixture(params=["auto", "throughput", "latency"])
+def kpath(sv, request):
+    """Runs the test on each kernel path (include/stellar_sigverify.h SV_PATH_*):
+    the one-lane prep + main kernels and the quad-per-signature latency kernel
+    must give identical verdicts."""
+    code = {"auto": sv.PATH_AUTO, "throughput": sv.PATH_THROUGHPUT, "latency": sv.PATH_LATENCY}[request.param]
+    prev = sv.set_kernel_path(code)
+    yield request.param
+    sv.set_kernel_path(prev)
+
+
 def _seed_msg(lo, hi):
     s, m = bytearray(), bytearray()
     for i in range(lo, hi):
@@ -56,7 +67,7 @@ def _gpu_sign(sv, dev, seeds, msgs):
 
 
 @pytest.mark.parametrize("name", ["intree", "valid", "msglen", "adversarial", "lattice_edge"])
-def test_golden_fixtures_variable_path(sv, dev, golden, name):
+def test_golden_fixtures_variable_path(sv, dev, golden, name, kpath):
     d = golden[name]
     out = sv.verify_batch(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"], device=0)
     bad = np.nonzero(out != d["verdict"])[0]
@@ -72,7 +83,7 @@ def test_intree_reference_expectations(sv, dev, golden):
     assert out[12:].sum() == 0  # all 196 Zcash vectors rejected
 
 
-def test_fixed32_path_on_golden_rows(sv, dev, golden):
+def test_fixed32_path_on_golden_rows(sv, dev, golden, kpath):
     for name in ("valid", "adversarial", "lattice_edge"):
         d = golden[name]
         rows = np.nonzero(d["msg_len"] == 32)[0]
@@ -81,7 +92,7 @@ def test_fixed32_path_on_golden_rows(sv, dev, golden):
         assert (out == d["verdict"][rows]).all(), name
 
 
-def test_fixed_256_reference_bench_shape(sv, dev, golden, oracle):
+def test_fixed_256_reference_bench_shape(sv, dev, golden, oracle, kpath):
     d = golden["valid"]
     rows = np.nonzero(d["msg_len"] == 256)[0]
     msgs = np.stack([d["msg"][o:o + 256] for o in d["msg_off"][rows]])
@@ -94,7 +105,7 @@ def test_fixed_256_reference_bench_shape(sv, dev, golden, oracle):
 
 
 @pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000, 4097])
-def test_device_api_ragged_sizes_and_bitmap(sv, dev, oracle, n):
+def test_device_api_ragged_sizes_and_bitmap(sv, dev, oracle, n, kpath):
     seeds, msgs = _seed_msg(10_000, 10_000 + n)
     tpk, tsig, tm = _gpu_sign(sv, dev, seeds, msgs)
     sig = tsig.cpu().numpy()
