@@ -55,6 +55,11 @@ __device__ unsigned long long g_clk[2][4096];
 #define X_ALIGN(i) asm volatile("v_alignbit_b32 %0, %0, %1, 26" : "+v"(acc[i]) : "v"(b));
 #define X_CND(i) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(acc[i]) : "v"(b));
 #define X_SHL32(i) asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(acc[i]));
+// select with a lane mask held in an ordinary SGPR pair (the form the compiler
+// emits for per-lane conditions computed once), and a DPP quad broadcast
+#define X_CNDS(i) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(acc[i]) : "v"(b) : "s40", "s41");
+#define X_DPP(i) asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf" : "=v"(acc[i]) : "v"(acc[(i + 1) & 7]));
+#define X_MUL19(i) asm volatile("v_mul_lo_u32 %0, %0, 19" : "+v"(acc[i]));
 #define X_MAD_VCC(i) asm volatile("v_mad_u64_u32 %0, vcc, %1, %1, %0" : "+v"(acc[i]) : "v"(a) : "vcc");
 
 K64(k_shr64, X_SHR64)
@@ -64,6 +69,9 @@ K32(k_add32, X_ADD32)
 K32(k_align, X_ALIGN)
 K32(k_cnd, X_CND)
 K32(k_shl32, X_SHL32)
+K32(k_cnds, X_CNDS)
+K32(k_dpp, X_DPP)
+K32(k_mul19, X_MUL19)
 K64(k_mad_vcc, X_MAD_VCC)
 
 // 8 chains, each writing its own SGPR pair s[10i..10i+1] (s[00:01] ... s[70:71])
@@ -182,6 +190,8 @@ int main() {
             {"v_and_b32", k_and, 1},           {"v_add_u32", k_add32, 1},
             {"v_alignbit_b32", k_align, 1},    {"v_cndmask_b32", k_cnd, 1},
             {"v_lshlrev_b32", k_shl32, 1},     {"v_mad_u64_u32 (vcc)", k_mad_vcc, 1},
+            {"v_cndmask_b32_e64 (sgpr mask)", k_cnds, 1}, {"v_mov_b32_dpp quad_perm", k_dpp, 1},
+            {"v_mul_lo_u32 x19", k_mul19, 1},
             {"v_mad_u64_u32 (8 sgpr pairs)", k_mad_spair, 1},
             {"carry step x8 chains", k_carry8, 3}, {"carry step 1 chain", k_carry1, 3},
             {"v_mad_u64_u32 1 dep chain", k_mad_dep, 1}};
