@@ -23,6 +23,9 @@
 #define SV_STAGE_A 1  // table_A entries via LDS-DMA prefetch (verify_core.h)
 #endif
 #define SV_WAVES_PER_SIMD 2
+#ifndef SV_MAIN_WAVES
+#define SV_MAIN_WAVES SV_WAVES_PER_SIMD
+#endif
 // 1: verify through the half-size equation (lattice.h, ~130 doublings per
 // signature); 0: the direct 253-bit ladder (sv_verify_kernel below).
 #ifndef SV_LATTICE
@@ -331,9 +334,9 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   SV_PHASE(4);
 }
 
-__global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_main_kernel(sv_cparams c) {
+__global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cparams c) {
   const sv_kparams& p = c.k;
-  __shared__ sv_u4 s_stage[SV_BLOCK / 64][2 * SV_LTAB_QUADS * 64];  // per-wave A and R entry stage
+  __shared__ sv_u4 s_stage[SV_BLOCK / 64][(SV_STAGE_ONE ? 1 : 2) * SV_LTAB_QUADS * 64];  // per-wave entry stage
   const uint32_t lane = threadIdx.x & 63u;
   sv_u4* stage = s_stage[threadIdx.x >> 6];
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

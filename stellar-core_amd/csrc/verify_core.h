@@ -594,6 +594,13 @@ SV_COLD void sv_lat_prepare(sv_lat_digits& D, const sv_lat& lat, const uint32_t 
   }
 }
 
+// 1: one 10-quad stage region per wave instead of two (10 KB): each entry is
+// DMA'd when the previous addition's entry has been read, so its latency hides
+// behind one addition instead of the window's doublings; frees LDS for more
+// waves per CU.
+#ifndef SV_STAGE_ONE
+#define SV_STAGE_ONE 1
+#endif
 // 1: the window's two base-point entries are also staged by LDS-DMA (into the
 // A and R regions once those entries have been read)
 #ifndef SV_LAT_STAGE_B
@@ -643,7 +650,9 @@ SV_HD void sv_lat_scalarmult(ge_p3& P, sv_lat_digits& D, int W, const sv_u4* tab
     if (STAGED) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       sv_stage_lentry(stage, tabA + (dA < 0 ? -dA : dA) * SV_LTAB_QUADS);
+#if !SV_STAGE_ONE
       sv_stage_lentry(stage + SV_LTAB_QUADS * 64, tabR + (dR < 0 ? -dR : dR) * SV_LTAB_QUADS);
+#endif
     }
 #endif
     SV_NOUNROLL for (int s = s0; s < nsteps; ++s) {
@@ -657,7 +666,17 @@ SV_HD void sv_lat_scalarmult(ge_p3& P, sv_lat_digits& D, int W, const sv_u4* tab
           const int32_t d = s == 4 ? dA : dR;
           neg = d < 0;
 #if defined(__HIP_DEVICE_COMPILE__)
-          if (STAGED) {
+          if (STAGED && SV_STAGE_ONE) {
+            // one region: the entry DMA'd for this step has landed; once it is
+            // read, the region receives the next addition's entry
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            sv_load_lentry(qa, qb, qz, qt, stage + __lane_id(), 64, neg);
+            if (s == 4 || bwin) {
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              if (s == 4) sv_stage_lentry(stage, tabR + (dR < 0 ? -dR : dR) * SV_LTAB_QUADS);
+              else sv_stage_bentry(stage, btab0, dB0);
+            }
+          } else if (STAGED) {
             // s = 4: the A and R entries (DMA'd at window start) have landed
             if (s == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             sv_u4* reg = stage + (s == 4 ? 0 : SV_LTAB_QUADS * 64);
@@ -680,7 +699,17 @@ SV_HD void sv_lat_scalarmult(ge_p3& P, sv_lat_digits& D, int W, const sv_u4* tab
           neg = d < 0;
           fe_1(qz);
 #if defined(__HIP_DEVICE_COMPILE__)
-          if (STAGED && SV_LAT_STAGE_B) {
+          if (STAGED && SV_STAGE_ONE) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const sv_u4* st = stage + __lane_id();
+            sv_load_fe3(qa, st, 64);
+            sv_load_fe3(qb, st + 3 * 64, 64);
+            sv_load_fe3(qt, st + 6 * 64, 64);
+            if (s == 6) {
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              sv_stage_bentry(stage, btab1, dB1);
+            }
+          } else if (STAGED && SV_LAT_STAGE_B) {
             // B0's DMA is older than B1's 9: vmcnt(9) covers it
             if (s == 6) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
