@@ -243,27 +243,14 @@ SV_HD void fe_sq2(fe& h, const fe& f) {
   fe_carry_wide(h, c);
   SV_FENCE();
 }
-// Unfenced forms: the next field operation may be scheduled into this one
-// (pairs of independent operations overlap one's carry chain with the other's
-// products, at the cost of ~20 more live VGPRs).
-SV_HD void fe_mul_nf(fe& h, const fe& f, const fe& g) {
-  uint64_t c[10];
-  fe_mul_cols<false>(c, f, g);
-  fe_carry_wide(h, c);
-}
-SV_HD void fe_sq_nf(fe& h, const fe& f) {
-  uint64_t c[10];
-  fe_sq_cols<false>(c, f);
-  fe_carry_wide(h, c);
-}
-
 // Two independent squarings / products in one scheduling region: the second
 // chain's products fill the first chain's serial carry-chain latency (used by
 // the prep kernel, which may run two decompressions side by side).
+template <bool DBL2 = false>  // DBL2: h2 = 2 f2^2
 SV_HD void fe_sq_x2(fe& h1, const fe& f1, fe& h2, const fe& f2) {
   uint64_t c1[10], c2[10];
   fe_sq_cols<false>(c1, f1);
-  fe_sq_cols<false>(c2, f2);
+  fe_sq_cols<DBL2>(c2, f2);
   fe_carry_wide(h1, c1);
   fe_carry_wide(h2, c2);
   SV_FENCE();

@@ -23,12 +23,13 @@
 
 #include "fe25519.h"
 
-// Overlap pairs of independent field operations in the hot formulas (A/B knobs)
-#ifndef SV_OVL_DBL
-#define SV_OVL_DBL 0
+// 1: the doubling's four squarings as two interleaved pairs (A/B knob)
+#ifndef SV_DBL_X2
+#define SV_DBL_X2 0
 #endif
-#ifndef SV_OVL_P1P1
-#define SV_OVL_P1P1 0
+// 1: the p1p1 conversions' products in interleaved pairs (A/B knob)
+#ifndef SV_P1P1_X2
+#define SV_P1P1_X2 0
 #endif
 
 struct ge_p2 { fe X, Y, Z; };
@@ -51,18 +52,16 @@ SV_HD void ge_p2_identity(ge_p2& p) {
 SV_HD void ge_dbl(ge_p1p1& r, const fe& X, const fe& Y, const fe& Z) {
   fe XX, YY, ZZ2, A, AA;
   fe_add(A, X, Y);
-#if SV_OVL_DBL
-  fe_sq_nf(AA, A);
+#if SV_DBL_X2
+  // squarings in interleaved pairs: one's carry chain overlaps the other's products
+  fe_sq_x2(AA, A, XX, X);
+  fe_sq_x2<true>(YY, Y, ZZ2, Z);
 #else
   fe_sq(AA, A);
-#endif
   fe_sq(XX, X);
-#if SV_OVL_DBL
-  fe_sq_nf(YY, Y);
-#else
   fe_sq(YY, Y);
-#endif
   fe_sq2(ZZ2, Z);
+#endif
   fe_add(r.Y, YY, XX);    // y^2 + x^2            M2
   fe_sub(r.Z, YY, XX);    // y^2 - x^2            M3
   fe_sub4(r.X, AA, r.Y);  // 2xy = (x+y)^2 - ..  M5
@@ -87,14 +86,16 @@ SV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
 // stale).  wantT is wave-uniform, so this is a scalar branch.  Operand order
 // matters: p.X (up to M5 after a doubling) is always the f operand.
 SV_HD void ge_p1p1_to_p3_opt(ge_p3& r, const ge_p1p1& p, bool wantT) {
-  if (wantT) fe_mul(r.T, p.X, p.Y);
-#if SV_OVL_P1P1
-  fe_mul_nf(r.X, p.X, p.T);
+#if SV_P1P1_X2
+  if (wantT) fe_mul_x2(r.T, p.X, p.Y, r.X, p.X, p.T);
+  else fe_mul(r.X, p.X, p.T);
+  fe_mul_x2(r.Y, p.Y, p.Z, r.Z, p.Z, p.T);
 #else
+  if (wantT) fe_mul(r.T, p.X, p.Y);
   fe_mul(r.X, p.X, p.T);
-#endif
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
+#endif
 }
 
 // r = p + q where the caller has already swapped q's (Y+X, Y-X) pair for a
