@@ -32,7 +32,6 @@
 #define SV_LATTICE 1
 #endif
 // base-point tables in the device buffer: e·B, then (SV_LATTICE) e·(2^128 B)
-#define SV_NBTAB (SV_LATTICE ? 2 : 1)
 
 struct sv_kparams {
   const sv_u4* pk;        // n x 32 B (2 quads)
@@ -175,7 +174,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_lat_ker
   sv_u4* tabA = p.ws + gtid * SV_SLOT_QUADS;
   sv_u4* tabR = tabA + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
   const sv_u4* btab0 = p.btab;
-  const sv_u4* btab1 = p.btab + SV_BTAB_ENTRIES * SV_BTAB_QUADS;
+  const sv_u4* btab1 = p.btab + SV_LBTAB_ENTRIES * SV_BTAB_QUADS;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
 
   for (uint64_t base = gtid - lane; base < p.n; base += stride) {
@@ -249,8 +248,10 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_lat_ker
 #ifndef SV_CHUNK
 #define SV_CHUNK (1u << 20)
 #endif
-#define SV_REC_QUADS 7
-// record flags (quad 6, .y)
+#define SV_REC_QUADS ((16 + 2 * SV_LB_DIGITS + 1 + 3) / 4)
+// record: dA[8] dR[8] dB0[SV_LB_DIGITS] dB1[SV_LB_DIGITS] flags (9 quads at radix 2^16)
+static_assert(16 + 2 * SV_LB_DIGITS + 1 <= 4 * SV_REC_QUADS, "digit record size");
+// record flags
 #define SV_REC_RNEG 1u
 #define SV_REC_TOP8A 2u
 #define SV_REC_TOP8R 4u
@@ -322,14 +323,19 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   sv_lat_prepare(D, lat, S, W);
   const uint32_t flags = (D.rneg ? SV_REC_RNEG : 0u) | (D.top8A ? SV_REC_TOP8A : 0u) |
                          (D.top8R ? SV_REC_TOP8R : 0u) | (ok ? SV_REC_OK : 0u);
+  uint32_t rw[4 * SV_REC_QUADS];
+  SV_UNROLL for (int k = 0; k < 4 * SV_REC_QUADS; ++k) rw[k] = 0u;
+  SV_UNROLL for (int k = 0; k < 8; ++k) {
+    rw[k] = D.dA[k];
+    rw[8 + k] = D.dR[k];
+  }
+  SV_UNROLL for (int k = 0; k < SV_LB_DIGITS; ++k) {
+    rw[16 + k] = (uint32_t)D.dB0[k];
+    rw[16 + SV_LB_DIGITS + k] = (uint32_t)D.dB1[k];
+  }
+  rw[16 + 2 * SV_LB_DIGITS] = flags;
   sv_u4* r = c.rec + li * SV_REC_QUADS;
-  r[0] = sv_u4{D.dA[0], D.dA[1], D.dA[2], D.dA[3]};
-  r[1] = sv_u4{D.dA[4], D.dA[5], D.dA[6], D.dA[7]};
-  r[2] = sv_u4{D.dR[0], D.dR[1], D.dR[2], D.dR[3]};
-  r[3] = sv_u4{D.dR[4], D.dR[5], D.dR[6], D.dR[7]};
-  r[4] = sv_u4{D.dB[0], D.dB[1], D.dB[2], D.dB[3]};
-  r[5] = sv_u4{D.dB[4], D.dB[5], D.dB[6], D.dB[7]};
-  r[6] = sv_u4{D.dB[8], flags, 0u, 0u};
+  SV_UNROLL for (int k = 0; k < SV_REC_QUADS; ++k) r[k] = sv_u4{rw[4 * k], rw[4 * k + 1], rw[4 * k + 2], rw[4 * k + 3]};
   if (lane == 0) c.wmax[li >> 6] = (uint32_t)W;
   SV_PHASE(4);
 }
@@ -341,7 +347,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cpa
   sv_u4* stage = s_stage[threadIdx.x >> 6];
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const sv_u4* btab0 = p.btab;
-  const sv_u4* btab1 = p.btab + SV_BTAB_ENTRIES * SV_BTAB_QUADS;
+  const sv_u4* btab1 = p.btab + SV_LBTAB_ENTRIES * SV_BTAB_QUADS;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = gtid - lane; base < c.cnt; base += stride) {
     const uint64_t li = base + lane;  // (slots exist up to the chunk's last full wave)
@@ -352,18 +358,24 @@ __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cpa
     sv_lat_digits D;
     bool pre_ok;
     {
-      const sv_u4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3], q4 = r[4], q5 = r[5], q6 = r[6];
-      D.dA[0] = q0.x; D.dA[1] = q0.y; D.dA[2] = q0.z; D.dA[3] = q0.w;
-      D.dA[4] = q1.x; D.dA[5] = q1.y; D.dA[6] = q1.z; D.dA[7] = q1.w;
-      D.dR[0] = q2.x; D.dR[1] = q2.y; D.dR[2] = q2.z; D.dR[3] = q2.w;
-      D.dR[4] = q3.x; D.dR[5] = q3.y; D.dR[6] = q3.z; D.dR[7] = q3.w;
-      D.dB[0] = q4.x; D.dB[1] = q4.y; D.dB[2] = q4.z; D.dB[3] = q4.w;
-      D.dB[4] = q5.x; D.dB[5] = q5.y; D.dB[6] = q5.z; D.dB[7] = q5.w;
-      D.dB[8] = q6.x;
-      D.rneg = (q6.y & SV_REC_RNEG) != 0;
-      D.top8A = (q6.y & SV_REC_TOP8A) != 0;
-      D.top8R = (q6.y & SV_REC_TOP8R) != 0;
-      pre_ok = (q6.y & SV_REC_OK) != 0;
+      uint32_t rw[4 * SV_REC_QUADS];
+      SV_UNROLL for (int k = 0; k < SV_REC_QUADS; ++k) {
+        const sv_u4 q = r[k];
+        rw[4 * k] = q.x; rw[4 * k + 1] = q.y; rw[4 * k + 2] = q.z; rw[4 * k + 3] = q.w;
+      }
+      SV_UNROLL for (int k = 0; k < 8; ++k) {
+        D.dA[k] = rw[k];
+        D.dR[k] = rw[8 + k];
+      }
+      SV_UNROLL for (int k = 0; k < SV_LB_DIGITS; ++k) {
+        D.dB0[k] = (int32_t)rw[16 + k];
+        D.dB1[k] = (int32_t)rw[16 + SV_LB_DIGITS + k];
+      }
+      const uint32_t flags = rw[16 + 2 * SV_LB_DIGITS];
+      D.rneg = (flags & SV_REC_RNEG) != 0;
+      D.top8A = (flags & SV_REC_TOP8A) != 0;
+      D.top8R = (flags & SV_REC_TOP8R) != 0;
+      pre_ok = (flags & SV_REC_OK) != 0;
     }
     const int W = (int)__builtin_amdgcn_readfirstlane(c.wmax[li >> 6]);
     ge_p3 P;
@@ -457,7 +469,7 @@ __global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
   __syncthreads();  // tables visible to the whole quad
 
   const sv_u4* btab0 = p.btab;
-  const sv_u4* btab1 = p.btab + SV_BTAB_ENTRIES * SV_BTAB_QUADS;
+  const sv_u4* btab1 = p.btab + SV_LBTAB_ENTRIES * SV_BTAB_QUADS;
   const uint32_t* tabA = &s_tab[sl][0][0][0];
   const uint32_t* tabR = &s_tab[sl][1][0][0];
   ge_p3 P;
@@ -470,15 +482,10 @@ __global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
       if (D.top8R) dR = 8;
     }
     if (D.rneg) dR = -dR;
-    const bool bwin = (w & 3) == 0 && (w >> 2) <= 8;
-    int32_t dB0 = 0, dB1 = 0;
+    int32_t dB0, dB1;
     fe b0, b1;
+    const bool bwin = sv_lat_bdigits(D, w, dB0, dB1);
     if (bwin) {
-      const uint32_t t = D.dB[8];
-      dB0 = ((int32_t)(t << 16)) >> 16;
-      dB1 = ((int32_t)t) >> 16;
-      SV_UNROLL for (int k = 8; k > 0; --k) D.dB[k] = D.dB[k - 1];
-      D.dB[0] = 0;
       // issued before the doublings: the loads land while they run
       qd_load_affine(b0, btab0 + (dB0 < 0 ? -dB0 : dB0) * SV_BTAB_QUADS, role, dB0 < 0);
       qd_load_affine(b1, btab1 + (dB1 < 0 ? -dB1 : dB1) * SV_BTAB_QUADS, role, dB1 < 0);
@@ -508,10 +515,14 @@ __global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
 
 __global__ void sv_btab_init_kernel(uint32_t* btab) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < SV_BTAB_ENTRIES) sv_btab_entry(btab + e * SV_BTAB_STRIDE, e);
 #if SV_LATTICE
-  else if (e < 2 * SV_BTAB_ENTRIES)
-    sv_btab_entry_shift(btab + e * SV_BTAB_STRIDE, e - SV_BTAB_ENTRIES, 128);
+  // table 0: e B (also the signer's table: it reads entries <= 2^(SV_B_BITS-1));
+  // table 1: e 2^128 B
+  if (e < SV_LBTAB_ENTRIES) sv_btab_entry_shift(btab + e * SV_BTAB_STRIDE, e, 0);
+  else if (e < 2 * SV_LBTAB_ENTRIES)
+    sv_btab_entry_shift(btab + e * SV_BTAB_STRIDE, e - SV_LBTAB_ENTRIES, 128);
+#else
+  if (e < SV_BTAB_ENTRIES) sv_btab_entry(btab + e * SV_BTAB_STRIDE, e);
 #endif
 }
 
@@ -578,11 +589,16 @@ size_t sv_ws_bytes(unsigned grid) {
 #endif
   return b;
 }
-size_t sv_btab_bytes(void) { return (size_t)SV_NBTAB * SV_BTAB_DWORDS * 4; }
+#if SV_LATTICE
+#define SV_BTAB_TOTAL (2 * SV_LBTAB_ENTRIES)
+#else
+#define SV_BTAB_TOTAL SV_BTAB_ENTRIES
+#endif
+size_t sv_btab_bytes(void) { return (size_t)SV_BTAB_TOTAL * SV_BTAB_STRIDE * 4; }
 int sv_block_threads(void) { return SV_BLOCK; }
 
 hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s) {
-  hipLaunchKernelGGL(sv_btab_init_kernel, dim3((SV_NBTAB * SV_BTAB_ENTRIES + 191) / 192), dim3(192), 0, s, d_btab);
+  hipLaunchKernelGGL(sv_btab_init_kernel, dim3((SV_BTAB_TOTAL + 191) / 192), dim3(192), 0, s, d_btab);
   return hipGetLastError();
 }
 

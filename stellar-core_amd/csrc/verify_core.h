@@ -462,6 +462,20 @@ SV_HD void sv_sign_lane(uint32_t pk[8], uint32_t sig[16], const uint32_t seed[8]
 // ------------------------------------------------ half-size path (lattice.h)
 // Base-point tables for the half-size path: entry e of table t is e·(2^(128 t) B)
 // (t = 0, 1), same 36-dword affine precomp layout as table_B.
+// Half-size path base-point digits: signed radix 2^SV_LB_BITS (a multiple of
+// the 4-bit window), digit j of each 128-bit half of (c1 S mod L) added at
+// window SV_LB_WIN * j; SV_LB_DIGITS digits cover 129+ bits (room for the
+// recoding carry).  Tables: e * 2^(128 t) * B for e in [0, 2^(SV_LB_BITS-1)].
+// Radix 2^20 (151 MB of tables) adds 14 base points per signature instead of
+// 18, but measured no faster than radix 2^16 (9.4 MB, L2/MALL-resident): the
+// saved additions come back as exposed latency of the DMA'd entries.
+#ifndef SV_LB_BITS
+#define SV_LB_BITS 16
+#endif
+#define SV_LB_WIN (SV_LB_BITS / 4)
+#define SV_LB_DIGITS ((128 + SV_LB_BITS) / SV_LB_BITS)
+#define SV_LBTAB_ENTRIES ((1 << (SV_LB_BITS - 1)) + 1)
+
 SV_HD void sv_btab_entry_shift(uint32_t out[SV_BTAB_STRIDE], int e, int shift) {
   const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                             0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
@@ -475,7 +489,7 @@ SV_HD void sv_btab_entry_shift(uint32_t out[SV_BTAB_STRIDE], int e, int shift) {
   ge_cached bc;
   ge_p3_to_cached(bc, B);
   fe_0(acc.X); fe_1(acc.Y); fe_1(acc.Z); fe_0(acc.T);
-  for (int bit = 15; bit >= 0; --bit) {
+  for (int bit = SV_LB_BITS - 1; bit >= 0; --bit) {
     ge_dbl(Q, acc.X, acc.Y, acc.Z);
     ge_p1p1_to_p3(acc, Q);
     if ((e >> bit) & 1) {
@@ -557,15 +571,44 @@ SV_HD void sv_digits_shift(uint32_t d[8], int k) {
 
 // Per-signature digit strings of (*) in lattice.h for W windows:
 //   dA: c0, dR: |c1| (signed radix 16, top digit = window W-1),
-//   dB[j] = digit j of (s mod 2^128) | digit j of (s >> 128) << 16 (radix 2^16,
-//   j = 0..8; digit j is added at window 4j).
+//   dB0[j], dB1[j] = signed radix-2^SV_LB_BITS digit j of (s mod 2^128) and of
+//   (s >> 128), s = c1 S mod L; digit j is added at window SV_LB_WIN * j.
 // A scalar of 4W-1 bits can carry out of digit W-1: that digit is then -8 and
 // the carry is 1, i.e. the top digit is really +8 (table entries go to 8);
 // top8A / top8R record it (4-bit two's complement digits stop at 7).
 struct sv_lat_digits {
-  uint32_t dA[8], dR[8], dB[9];
+  uint32_t dA[8], dR[8];
+  int32_t dB0[SV_LB_DIGITS], dB1[SV_LB_DIGITS];
   bool rneg, top8A, top8R;
 };
+
+// Signed radix-2^SV_LB_BITS digits of a 128-bit x: d_j in [-2^(B-1), 2^(B-1)).
+SV_HD void sc_digits_lb(int32_t d[SV_LB_DIGITS], const uint32_t x[4]) {
+  uint32_t carry = 0;
+  SV_UNROLL for (int j = 0; j < SV_LB_DIGITS; ++j) {
+    const int o = j * SV_LB_BITS, q = o >> 5, r = o & 31;
+    uint32_t v = q < 4 ? (x[q] >> r) : 0u;
+    if (r != 0 && q + 1 < 4 && r + SV_LB_BITS > 32) v |= x[q + 1] << (32 - r);
+    v = (v & ((1u << SV_LB_BITS) - 1u)) + carry;
+    carry = (v + (1u << (SV_LB_BITS - 1))) >> SV_LB_BITS;  // v >= 2^(B-1)
+    d[j] = (int32_t)v - (int32_t)(carry << SV_LB_BITS);
+  }
+}
+
+// The window's base-point digits, popped from the top (windows run MSB
+// first, so the first window carrying one is SV_LB_WIN * (SV_LB_DIGITS - 1)).
+SV_HD bool sv_lat_bdigits(sv_lat_digits& D, int w, int32_t& dB0, int32_t& dB1) {
+  dB0 = dB1 = 0;
+  if (w % SV_LB_WIN != 0 || w / SV_LB_WIN >= SV_LB_DIGITS) return false;
+  dB0 = D.dB0[SV_LB_DIGITS - 1];
+  dB1 = D.dB1[SV_LB_DIGITS - 1];
+  SV_UNROLL for (int k = SV_LB_DIGITS - 1; k > 0; --k) {
+    D.dB0[k] = D.dB0[k - 1];
+    D.dB1[k] = D.dB1[k - 1];
+  }
+  D.dB0[0] = D.dB1[0] = 0;
+  return true;
+}
 
 SV_COLD void sv_lat_prepare(sv_lat_digits& D, const sv_lat& lat, const uint32_t S[8], int W) {
   sc_digits_r16(D.dA, lat.c0);
@@ -579,19 +622,10 @@ SV_COLD void sv_lat_prepare(sv_lat_digits& D, const sv_lat& lat, const uint32_t 
     D.top8A = D.top8R = false;
   }
   D.rneg = lat.c1neg;
-  uint32_t s[8], lo[8], hi[8], d0[8], d1[8];
+  uint32_t s[8];
   sc_mul_signed(s, lat.c1, lat.c1neg, S);
-  SV_UNROLL for (int i = 0; i < 8; ++i) {
-    lo[i] = i < 4 ? s[i] : 0u;
-    hi[i] = i < 4 ? s[4 + i] : 0u;
-  }
-  sc_digits_r65536(d0, lo);
-  sc_digits_r65536(d1, hi);
-  SV_UNROLL for (int j = 0; j < 9; ++j) {
-    const uint32_t a = (d0[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-    const uint32_t b = (d1[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-    D.dB[j] = a | (b << 16);
-  }
+  sc_digits_lb(D.dB0, s);      // s mod 2^128
+  sc_digits_lb(D.dB1, s + 4);  // s >> 128 (< 2^125)
 }
 
 // 1: one 10-quad stage region per wave instead of two (10 KB): each entry is
@@ -635,15 +669,8 @@ SV_HD void sv_lat_scalarmult(ge_p3& P, sv_lat_digits& D, int W, const sv_u4* tab
       if (D.top8R) dR = 8;
     }
     if (D.rneg) dR = -dR;
-    const bool bwin = (w & 3) == 0 && (w >> 2) <= 8;
-    int32_t dB0 = 0, dB1 = 0;
-    if (bwin) {
-      const uint32_t t = D.dB[8];
-      dB0 = ((int32_t)(t << 16)) >> 16;
-      dB1 = ((int32_t)t) >> 16;
-      SV_UNROLL for (int i = 8; i > 0; --i) D.dB[i] = D.dB[i - 1];
-      D.dB[0] = 0;
-    }
+    int32_t dB0, dB1;
+    const bool bwin = sv_lat_bdigits(D, w, dB0, dB1);
     const int nsteps = bwin ? 8 : 6;
     const int s0 = (w == W - 1) ? 4 : 0;
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -14,21 +14,38 @@
 static std::vector<uint32_t> g_btab;
 static std::once_flag g_once;
 
-static std::vector<uint32_t> g_btab1;  // e·(2^128 B) for the half-size path
+// Half-size path tables e·B and e·(2^128 B), e <= 2^(SV_LB_BITS-1): over a
+// million entries, so the host build fills them lazily, only the entries a
+// signature's digits select (lat_need_btab) -- test setup only.
+static std::vector<uint32_t> g_lb[2];
+static std::vector<uint8_t> g_lb_done[2];
 
 static void init_btab() {
   g_btab.assign(SV_BTAB_DWORDS + 8, 0);
-  g_btab1.assign(SV_BTAB_DWORDS + 8, 0);
   // (the build container has 8 CPUs; the tables are test setup only)
   std::vector<std::thread> th;
   for (int t = 0; t < 8; ++t)
     th.emplace_back([t] {
-      for (int e = t; e < SV_BTAB_ENTRIES; e += 8) {
-        sv_btab_entry(&g_btab[e * SV_BTAB_STRIDE], e);
-        sv_btab_entry_shift(&g_btab1[e * SV_BTAB_STRIDE], e, 128);
-      }
+      for (int e = t; e < SV_BTAB_ENTRIES; e += 8) sv_btab_entry(&g_btab[e * SV_BTAB_STRIDE], e);
     });
   for (auto& x : th) x.join();
+  for (int t = 0; t < 2; ++t) {
+    g_lb[t].assign((size_t)SV_LBTAB_ENTRIES * SV_BTAB_STRIDE + 8, 0);
+    g_lb_done[t].assign(SV_LBTAB_ENTRIES, 0);
+  }
+}
+
+static void lat_need_btab(const sv_lat_digits& D) {
+  for (int j = 0; j < SV_LB_DIGITS; ++j) {
+    const int32_t d[2] = {D.dB0[j], D.dB1[j]};
+    for (int t = 0; t < 2; ++t) {
+      const int e = d[t] < 0 ? -d[t] : d[t];
+      if (!g_lb_done[t][e]) {
+        sv_btab_entry_shift(&g_lb[t][(size_t)e * SV_BTAB_STRIDE], e, 128 * t);
+        g_lb_done[t][e] = 1;
+      }
+    }
+  }
 }
 
 static void load_words(uint32_t w[8], const uint8_t* b) { memcpy(w, b, 32); }
@@ -202,8 +219,9 @@ extern "C" void hc_verify_batch_lat(const uint8_t* pk, const uint8_t* sig, const
     if (W < wmin) W = wmin;
     sv_lat_digits D;
     sv_lat_prepare(D, lat, S, W);
+    lat_need_btab(D);
     ge_p3 P;
-    sv_lat_scalarmult(P, D, W, tabA, tabR, (const sv_u4*)g_btab.data(), (const sv_u4*)g_btab1.data());
+    sv_lat_scalarmult(P, D, W, tabA, tabR, (const sv_u4*)g_lb[0].data(), (const sv_u4*)g_lb[1].data());
     verdict[i] = (ok && sv_is_identity(P)) ? 1 : 0;
   }
 }
