@@ -131,8 +131,13 @@ def _ptr(a: np.ndarray) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
 
 
-def _opts(device: int = -1, max_devices: int = 0):
-    o = sv_opts(ctypes.sizeof(sv_opts), device, max_devices, 0)
+# sv_opts.flags kernel-path requests (include/stellar_sigverify.h)
+FLAG_PATH = {None: 0, "auto": 0, "throughput": 0x1, "latency": 0x2}
+
+
+def _opts(device: int = -1, max_devices: int = 0, path=None):
+    o = sv_opts(ctypes.sizeof(sv_opts), device, max_devices, FLAG_PATH[path] if isinstance(path, (str, type(None)))
+                else int(path))
     return ctypes.byref(o)
 
 
@@ -153,11 +158,12 @@ def _u8(a, shape_tail: int) -> np.ndarray:
     return a.reshape(-1, shape_tail)
 
 
-def verify_batch(pk, sig, msg, msg_off, msg_len, device: int = -1, max_devices: int = 0) -> np.ndarray:
+def verify_batch(pk, sig, msg, msg_off, msg_len, device: int = -1, max_devices: int = 0, path=None) -> np.ndarray:
     """Variable-length batch: message i = msg[msg_off[i]:msg_off[i]+msg_len[i]].
 
     Returns a uint8 verdict array (1 = valid), bit-identical to libsodium's
-    crypto_sign_verify_detached on every row."""
+    crypto_sign_verify_detached on every row.  path: None / "auto",
+    "throughput" or "latency" (sv_opts.flags; verdicts are identical)."""
     lib = load_library()
     pk = _u8(pk, 32)
     sig = _u8(sig, 64)
@@ -175,7 +181,7 @@ def verify_batch(pk, sig, msg, msg_off, msg_len, device: int = -1, max_devices: 
         raise ValueError("message range out of bounds")
     out = np.zeros(n, np.uint8)
     _check(lib.sv_ed25519_verify_batch(_ptr(pk), _ptr(sig), _ptr(msg), _ptr(off), _ptr(ln), n, _ptr(out),
-                                       _opts(device, max_devices)))
+                                       _opts(device, max_devices, path)))
     return out
 
 
@@ -238,7 +244,7 @@ def verify_messages(pk, sig, messages: Sequence[bytes], **kw) -> np.ndarray:
     return verify_batch(pk, sig, buf, off, lens, **kw)
 
 
-def verify_fixed(pk, sig, msg, msg_len: int = 32, device: int = -1, max_devices: int = 0) -> np.ndarray:
+def verify_fixed(pk, sig, msg, msg_len: int = 32, device: int = -1, max_devices: int = 0, path=None) -> np.ndarray:
     """Fixed-length batch (msg is n x msg_len bytes); msg_len 32 = tx contents hashes."""
     lib = load_library()
     pk = _u8(pk, 32)
@@ -251,7 +257,7 @@ def verify_fixed(pk, sig, msg, msg_len: int = 32, device: int = -1, max_devices:
         msg = np.zeros(1, np.uint8)
     out = np.zeros(n, np.uint8)
     _check(lib.sv_ed25519_verify_batch_fixed(_ptr(pk), _ptr(sig), _ptr(msg), msg_len, n, _ptr(out),
-                                             _opts(device, max_devices)))
+                                             _opts(device, max_devices, path)))
     return out
 
 

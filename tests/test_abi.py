@@ -91,3 +91,13 @@ def test_python_binding_validates_shapes(sv):
     with pytest.raises(ValueError):
         sv.verify_batch(np.zeros((2, 32), np.uint8), np.zeros((2, 64), np.uint8), np.zeros(4, np.uint8),
                         [0, 3], [1, 2])
+
+
+def test_kernel_path_setter_validates(sv):
+    """sv_set_kernel_path accepts SV_PATH_AUTO/THROUGHPUT/LATENCY, returns the
+    previous default, and rejects anything else (no GPU needed)."""
+    prev = sv.set_kernel_path(sv.PATH_LATENCY)
+    assert sv.set_kernel_path(sv.PATH_THROUGHPUT) == sv.PATH_LATENCY
+    assert sv.set_kernel_path(prev) == sv.PATH_THROUGHPUT
+    with pytest.raises(sv.SigVerifyError):
+        sv.set_kernel_path(7)

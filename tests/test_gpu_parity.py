@@ -74,6 +74,17 @@ def test_golden_fixtures_variable_path(sv, dev, golden, name, kpath):
     assert len(bad) == 0, [(int(i), str(d["class_names"][d["cls"][i]])) for i in bad[:10]]
 
 
+def test_per_call_path_flags(sv, dev, golden):
+    """sv_opts.flags selects the kernel path per call; both give libsodium's
+    verdicts; contradictory flags are rejected."""
+    d = golden["adversarial"]
+    for path in ("throughput", "latency"):
+        out = sv.verify_batch(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"], device=0, path=path)
+        assert (out == d["verdict"]).all(), path
+    with pytest.raises(sv.SigVerifyError):
+        sv.verify_batch(d["pk"][:1], d["sig"][:1], d["msg"], d["msg_off"][:1], d["msg_len"][:1], device=0, path=3)
+
+
 def test_intree_reference_expectations(sv, dev, golden):
     d = golden["intree"]
     out = sv.verify_batch(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"])
