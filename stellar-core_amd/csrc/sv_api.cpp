@@ -83,6 +83,32 @@ struct DevBuf {
   }
 };
 
+// Pinned host staging (hipHostMalloc): one H2D copy per batch instead of one
+// pageable copy per input array.
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return SV_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return fail(SV_ERR_ALLOC, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    }
+    cap = want;
+    return SV_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 struct Device {
   int id = -1;
   bool ready = false;  // resources created lazily on first use (under mu)
@@ -94,6 +120,8 @@ struct Device {
   hipEvent_t dep_in = nullptr, dep_out = nullptr;
   std::mutex mu;
   DevBuf pk, sig, msg, off, len, verdict, keys;
+  DevBuf in;          // staged batch: pk | sig | [off | len] | msg
+  HostBuf h_in, h_out;
   // timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   std::vector<uint64_t> pending_n;
@@ -219,49 +247,57 @@ int host_slice(Device& D, const uint8_t* pk, const uint8_t* sig, const uint8_t* 
   SV_HIP(hipSetDevice(D.id));
   int rc;
   if ((rc = ready_locked(D))) return rc;
-  if ((rc = D.pk.ensure(n * 32)) || (rc = D.sig.ensure(n * 64))) return rc;
-  if (verdict && (rc = D.verdict.ensure(n))) return rc;
-  if (keys && (rc = D.keys.ensure(n * 32))) return rc;
-  SV_HIP(hipMemcpyAsync(D.pk.p, pk, n * 32, hipMemcpyHostToDevice, D.stream));
-  SV_HIP(hipMemcpyAsync(D.sig.p, sig, n * 64, hipMemcpyHostToDevice, D.stream));
-  int mode;
-  std::vector<uint64_t> offs;
-  std::vector<uint8_t> packed;
+  // one pinned staging image, one H2D copy:
+  //   pk (32 n) | sig (64 n) | fixed: msg (n L)  or  var: off (8 n) | len (4 n) | packed msgs
+  // (pk, sig, and a fixed-length msg block stay 16-byte aligned)
+  const size_t o_sig = 32 * n, o_var = 96 * n;
+  size_t total_msg = 0;
   if (fixed_len != 0) {
-    if ((rc = D.msg.ensure((size_t)n * fixed_len))) return rc;
-    if (n * (size_t)fixed_len)
-      SV_HIP(hipMemcpyAsync(D.msg.p, msg, n * (size_t)fixed_len, hipMemcpyHostToDevice, D.stream));
+    total_msg = n * (size_t)fixed_len;
+  } else {
+    for (size_t i = 0; i < n; ++i) total_msg += msg_len[i];
+  }
+  const size_t o_off = o_var, o_len = o_var + 8 * n;
+  const size_t o_msg = fixed_len != 0 ? o_var : o_var + 12 * n;
+  const size_t bytes = o_msg + std::max<size_t>(total_msg, 1);
+  if ((rc = D.in.ensure(bytes)) || (rc = D.h_in.ensure(bytes))) return rc;
+  if (verdict && ((rc = D.verdict.ensure(n)) || (rc = D.h_out.ensure(n)))) return rc;
+  if (keys && (rc = D.keys.ensure(n * 32))) return rc;
+  uint8_t* h = (uint8_t*)D.h_in.p;
+  memcpy(h, pk, n * 32);
+  memcpy(h + o_sig, sig, n * 64);
+  int mode;
+  if (fixed_len != 0) {
+    if (total_msg) memcpy(h + o_msg, msg, total_msg);
     mode = (fixed_len == 32) ? 0 : 2;
   } else {
     // pack this slice's messages contiguously (offsets may be arbitrary)
-    size_t total = 0;
-    for (size_t i = 0; i < n; ++i) total += msg_len[i];
-    packed.resize(std::max<size_t>(total, 1));
-    offs.resize(n);
+    uint64_t* offs = (uint64_t*)(h + o_off);
     size_t pos = 0;
     for (size_t i = 0; i < n; ++i) {
       offs[i] = pos;
-      if (msg_len[i]) memcpy(packed.data() + pos, msg + msg_off[i], msg_len[i]);
+      if (msg_len[i]) memcpy(h + o_msg + pos, msg + msg_off[i], msg_len[i]);
       pos += msg_len[i];
     }
-    if ((rc = D.msg.ensure(packed.size())) || (rc = D.off.ensure(n * 8)) || (rc = D.len.ensure(n * 4))) return rc;
-    SV_HIP(hipMemcpyAsync(D.msg.p, packed.data(), packed.size(), hipMemcpyHostToDevice, D.stream));
-    SV_HIP(hipMemcpyAsync(D.off.p, offs.data(), n * 8, hipMemcpyHostToDevice, D.stream));
-    SV_HIP(hipMemcpyAsync(D.len.p, msg_len, n * 4, hipMemcpyHostToDevice, D.stream));
+    memcpy(h + o_len, msg_len, n * 4);
     mode = 1;
   }
+  SV_HIP(hipMemcpyAsync(D.in.p, h, bytes, hipMemcpyHostToDevice, D.stream));
+  uint8_t* d = (uint8_t*)D.in.p;
+  const uint64_t* d_off = fixed_len ? nullptr : (const uint64_t*)(d + o_off);
+  const uint32_t* d_len = fixed_len ? nullptr : (const uint32_t*)(d + o_len);
   if (keys) {
-    SV_HIP(sv_launch_hash(0, D.grid * 2, D.pk.p, D.sig.p, D.msg.p, (const uint64_t*)D.off.p,
-                          (const uint32_t*)D.len.p, fixed_len, n, D.keys.p, D.stream));
+    SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + o_sig, d + o_msg, d_off, d_len, fixed_len, n, D.keys.p, D.stream));
     SV_HIP(hipMemcpyAsync(keys, D.keys.p, n * 32, hipMemcpyDeviceToHost, D.stream));
   }
   if (verdict) {
-    if ((rc = launch_locked(D, mode, path, D.pk.p, D.sig.p, D.msg.p, (const uint64_t*)D.off.p,
-                            (const uint32_t*)D.len.p, fixed_len, n, D.verdict.p, nullptr)))
+    if ((rc = launch_locked(D, mode, path, d, d + o_sig, d + o_msg, d_off, d_len, fixed_len, n, D.verdict.p,
+                            nullptr)))
       return rc;
-    SV_HIP(hipMemcpyAsync(verdict, D.verdict.p, n, hipMemcpyDeviceToHost, D.stream));
+    SV_HIP(hipMemcpyAsync(D.h_out.p, D.verdict.p, n, hipMemcpyDeviceToHost, D.stream));
   }
-  SV_HIP(hipStreamSynchronize(D.stream));  // packed/offs must outlive the copies
+  SV_HIP(hipStreamSynchronize(D.stream));  // the staging buffers are reused by the next call
+  if (verdict) memcpy(verdict, D.h_out.p, n);
   return SV_OK;
 }
 
@@ -397,6 +433,7 @@ void sv_shutdown(void) {
     }
     D->pk.release(); D->sig.release(); D->msg.release();
     D->off.release(); D->len.release(); D->verdict.release(); D->keys.release();
+    D->in.release(); D->h_in.release(); D->h_out.release();
     if (D->ws) (void)hipFree(D->ws);
     if (D->btab) (void)hipFree(D->btab);
     if (D->dep_in) (void)hipEventDestroy(D->dep_in);
