@@ -243,31 +243,6 @@ SV_HD void fe_sq2(fe& h, const fe& f) {
   fe_carry_wide(h, c);
   SV_FENCE();
 }
-// Two independent squarings / products in one scheduling region: the second
-// chain's products fill the first chain's serial carry-chain latency (used by
-// the prep kernel, which may run two decompressions side by side).
-template <bool DBL2 = false>  // DBL2: h2 = 2 f2^2
-SV_HD void fe_sq_x2(fe& h1, const fe& f1, fe& h2, const fe& f2) {
-  uint64_t c1[10], c2[10];
-  fe_sq_cols<false>(c1, f1);
-  fe_sq_cols<DBL2>(c2, f2);
-  fe_carry_wide(h1, c1);
-  fe_carry_wide(h2, c2);
-  SV_FENCE();
-}
-SV_HD void fe_mul_x2(fe& h1, const fe& f1, const fe& g1, fe& h2, const fe& f2, const fe& g2) {
-  uint64_t c1[10], c2[10];
-  fe_mul_cols<false>(c1, f1, g1);
-  fe_mul_cols<false>(c2, f2, g2);
-  fe_carry_wide(h1, c1);
-  fe_carry_wide(h2, c2);
-  SV_FENCE();
-}
-SV_HD void fe_sqn_x2(fe& h1, const fe& f1, fe& h2, const fe& f2, int n) {
-  fe_sq_x2(h1, f1, h2, f2);
-  SV_NOUNROLL for (int i = 1; i < n; ++i) fe_sq_x2(h1, h1, h2, h2);
-}
-
 // n successive squarings (rolled loop: keeps the code object small)
 SV_HD void fe_sqn(fe& h, const fe& f, int n) {
   fe_sq(h, f);
@@ -364,33 +339,6 @@ SV_COLD void fe_pow22523(fe& h, const fe& z) {
   fe_pow_2_250_1(z250, z11, z);
   fe_sqn(z250, z250, 2);
   fe_mul(h, z250, z);
-}
-
-// (z1, z2)^((p-5)/8), the two chains interleaved (same chain as fe_pow22523)
-SV_COLD void fe_pow22523_x2(fe& h1, const fe& z1, fe& h2, const fe& z2) {
-  fe a0, a1, a9, a5, a10, a20, a50, a100, aa, b0, b1, b9, b5, b10, b20, b50, b100, bb;
-  fe_sq_x2(a0, z1, b0, z2);               // z^2
-  fe_sqn_x2(a1, a0, b1, b0, 2);           // z^8
-  fe_mul_x2(a9, a1, z1, b9, b1, z2);      // z^9
-  fe_mul_x2(aa, a9, a0, bb, b9, b0);      // z^11
-  fe_sq_x2(aa, aa, bb, bb);               // z^22
-  fe_mul_x2(a5, aa, a9, b5, bb, b9);      // 2^5 - 1
-  fe_sqn_x2(aa, a5, bb, b5, 5);
-  fe_mul_x2(a10, aa, a5, b10, bb, b5);    // 2^10 - 1
-  fe_sqn_x2(aa, a10, bb, b10, 10);
-  fe_mul_x2(a20, aa, a10, b20, bb, b10);  // 2^20 - 1
-  fe_sqn_x2(aa, a20, bb, b20, 20);
-  fe_mul_x2(aa, aa, a20, bb, bb, b20);    // 2^40 - 1
-  fe_sqn_x2(aa, aa, bb, bb, 10);
-  fe_mul_x2(a50, aa, a10, b50, bb, b10);  // 2^50 - 1
-  fe_sqn_x2(aa, a50, bb, b50, 50);
-  fe_mul_x2(a100, aa, a50, b100, bb, b50);  // 2^100 - 1
-  fe_sqn_x2(aa, a100, bb, b100, 100);
-  fe_mul_x2(aa, aa, a100, bb, bb, b100);  // 2^200 - 1
-  fe_sqn_x2(aa, aa, bb, bb, 50);
-  fe_mul_x2(aa, aa, a50, bb, bb, b50);    // 2^250 - 1
-  fe_sqn_x2(aa, aa, bb, bb, 2);
-  fe_mul_x2(h1, aa, z1, h2, bb, z2);      // 2^252 - 3
 }
 
 // z^(p-2) = z^(2^255 - 21)

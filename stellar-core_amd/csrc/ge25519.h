@@ -23,14 +23,6 @@
 
 #include "fe25519.h"
 
-// 1: the doubling's four squarings as two interleaved pairs (A/B knob)
-#ifndef SV_DBL_X2
-#define SV_DBL_X2 0
-#endif
-// 1: the p1p1 conversions' products in interleaved pairs (A/B knob)
-#ifndef SV_P1P1_X2
-#define SV_P1P1_X2 0
-#endif
 
 struct ge_p2 { fe X, Y, Z; };
 struct ge_p3 { fe X, Y, Z, T; };
@@ -52,16 +44,10 @@ SV_HD void ge_p2_identity(ge_p2& p) {
 SV_HD void ge_dbl(ge_p1p1& r, const fe& X, const fe& Y, const fe& Z) {
   fe XX, YY, ZZ2, A, AA;
   fe_add(A, X, Y);
-#if SV_DBL_X2
-  // squarings in interleaved pairs: one's carry chain overlaps the other's products
-  fe_sq_x2(AA, A, XX, X);
-  fe_sq_x2<true>(YY, Y, ZZ2, Z);
-#else
   fe_sq(AA, A);
   fe_sq(XX, X);
   fe_sq(YY, Y);
   fe_sq2(ZZ2, Z);
-#endif
   fe_add(r.Y, YY, XX);    // y^2 + x^2            M2
   fe_sub(r.Z, YY, XX);    // y^2 - x^2            M3
   fe_sub4(r.X, AA, r.Y);  // 2xy = (x+y)^2 - ..  M5
@@ -86,16 +72,10 @@ SV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
 // stale).  wantT is wave-uniform, so this is a scalar branch.  Operand order
 // matters: p.X (up to M5 after a doubling) is always the f operand.
 SV_HD void ge_p1p1_to_p3_opt(ge_p3& r, const ge_p1p1& p, bool wantT) {
-#if SV_P1P1_X2
-  if (wantT) fe_mul_x2(r.T, p.X, p.Y, r.X, p.X, p.T);
-  else fe_mul(r.X, p.X, p.T);
-  fe_mul_x2(r.Y, p.Y, p.Z, r.Z, p.Z, p.T);
-#else
   if (wantT) fe_mul(r.T, p.X, p.Y);
   fe_mul(r.X, p.X, p.T);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
-#endif
 }
 
 // r = p + q where the caller has already swapped q's (Y+X, Y-X) pair for a
@@ -195,39 +175,6 @@ SV_COLD bool ge_frombytes(ge_p3& h, const uint32_t w[8], bool negate) {
   fe_mul(h.X, h.X, v3);
   fe_mul(h.X, h.X, u);  // u v^3 (u v^7)^((p-5)/8)
   return ge_frombytes_finish(h, u, v, w, negate);
-}
-
-// Two decompressions (-P1, -P2) with their exponentiation chains interleaved;
-// per point exactly ge_frombytes(.., negate = true).
-SV_COLD void ge_frombytes_neg_x2(ge_p3& h1, bool& ok1, const uint32_t w1[8], ge_p3& h2, bool& ok2,
-                                 const uint32_t w2[8]) {
-  fe u1, v1, c1, u2, v2, c2, one, d;
-  fe_1(one);
-  fe_const_d(d);
-  fe_frombytes(h1.Y, w1);
-  fe_frombytes(h2.Y, w2);
-  fe_1(h1.Z);
-  fe_1(h2.Z);
-  fe_sq_x2(u1, h1.Y, u2, h2.Y);
-  fe_mul_x2(v1, u1, d, v2, u2, d);
-  fe_sub(u1, u1, one);
-  fe_weak(u1);
-  fe_sub(u2, u2, one);
-  fe_weak(u2);
-  fe_add(v1, v1, one);
-  fe_weak(v1);
-  fe_add(v2, v2, one);
-  fe_weak(v2);
-  fe_sq_x2(c1, v1, c2, v2);
-  fe_mul_x2(c1, c1, v1, c2, c2, v2);  // v^3
-  fe_sq_x2(h1.X, c1, h2.X, c2);
-  fe_mul_x2(h1.X, h1.X, v1, h2.X, h2.X, v2);
-  fe_mul_x2(h1.X, h1.X, u1, h2.X, h2.X, u2);  // u v^7
-  fe_pow22523_x2(h1.X, h1.X, h2.X, h2.X);
-  fe_mul_x2(h1.X, h1.X, c1, h2.X, h2.X, c2);
-  fe_mul_x2(h1.X, h1.X, u1, h2.X, h2.X, u2);  // u v^3 (u v^7)^((p-5)/8)
-  ok1 = ge_frombytes_finish(h1, u1, v1, w1, true);
-  ok2 = ge_frombytes_finish(h2, u2, v2, w2, true);
 }
 
 // canonical encoding of a projective point given 1/Z (8 little-endian words)

@@ -767,11 +767,6 @@ SV_HD bool sv_is_identity(const ge_p3& P) {
   return fe_iszero(P.X) && fe_iszero(d);
 }
 
-// 1: A and R are decompressed with interleaved exponentiation chains
-#ifndef SV_DECODE_X2
-#define SV_DECODE_X2 0
-#endif
-
 // Steps (1)-(5) of libsodium plus the decode of R (lattice.h), the Euclid
 // reduction and the table build.  Returns the pre-verdict and the lane's
 // window count in *W_lane; the caller picks the wave's W >= every W_lane.
@@ -780,14 +775,8 @@ SV_COLD bool sv_lat_pre(sv_lat& lat, const uint32_t A[8], const uint32_t R[8], c
   bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
             sv_point_canonical(R);
   ge_p3 negA, negR;
-#if SV_DECODE_X2
-  bool okA, okR;
-  ge_frombytes_neg_x2(negA, okA, A, negR, okR, R);
-  ok = ok && okA && okR;
-#else
   ok = ge_frombytes(negA, A, true) && ok;
   ok = ge_frombytes(negR, R, true) && ok;
-#endif
   uint32_t h[8];
   sc_reduce512(h, hram);
   sc_lattice_reduce(lat, h);
