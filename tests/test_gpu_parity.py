@@ -167,8 +167,9 @@ def test_gpu_signer_dataset_digest_64k(sv, dev):
 
 
 def test_full_size_properties_1m(sv, dev, oracle):
-    """2^20 + 17 signatures: all valid accepted, exactly the corrupted 1% rejected,
-    64 random rows agree with the oracle (size-independent properties)."""
+    """2^20 + 17 signatures (two prep/main chunks): all valid accepted, exactly
+    the corrupted 1% rejected, verdict bytes and bitmap agree, 64 random rows
+    agree with the oracle (size-independent properties)."""
     n = (1 << 20) + 17
     rng = np.random.default_rng(2025)
     seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
@@ -183,12 +184,17 @@ def test_full_size_properties_1m(sv, dev, oracle):
     sig = tsig.cpu().numpy()
     sig[bad, 32 + rng.integers(0, 32, len(bad))] ^= 0x01
     tsig.copy_(torch.from_numpy(sig))
-    sv.verify_device(0, tpk.data_ptr(), tsig.data_ptr(), tm.data_ptr(), n, tv.data_ptr(), 0, st)
+    tb = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    sv.verify_device(0, tpk.data_ptr(), tsig.data_ptr(), tm.data_ptr(), n, tv.data_ptr(), tb.data_ptr(), st)
     torch.cuda.synchronize(dev)
     got = tv.cpu().numpy()
     want = np.ones(n, np.uint8)
     want[bad] = 0
     assert np.array_equal(got, want)
+    # the ballot bitmap across the 2^20-signature chunk boundary
+    words = tb.cpu().numpy().view(np.uint64)
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:n]
+    assert np.array_equal(bits, want)
     pk = tpk.cpu().numpy()
     for i in rng.choice(n, 64, replace=False):
         ok = oracle.oracle_ed25519_verify(sig[i].tobytes(), msgs[i].tobytes(), 32, pk[i].tobytes()) == 0
