@@ -463,17 +463,22 @@ SV_HD void sv_sign_lane(uint32_t pk[8], uint32_t sig[16], const uint32_t seed[8]
 // Base-point tables for the half-size path: entry e of table t is e·(2^(128 t) B)
 // (t = 0, 1), same 36-dword affine precomp layout as table_B.
 // Half-size path base-point digits: signed radix 2^SV_LB_BITS (a multiple of
-// the 4-bit window), digit j of each 128-bit half of (c1 S mod L) added at
-// window SV_LB_WIN * j; SV_LB_DIGITS digits cover 129+ bits (room for the
-// recoding carry).  Tables: e * 2^(128 t) * B for e in [0, 2^(SV_LB_BITS-1)].
-// Radix 2^20 (151 MB of tables) adds 14 base points per signature instead of
-// 18, but measured no faster than radix 2^16 (9.4 MB, L2/MALL-resident): the
-// saved additions come back as exposed latency of the DMA'd entries.
+// the 4-bit window, dividing 128).  s = c1 S mod L (< 2^253) is recoded as ONE
+// 256-bit signed digit string; digits 0..SV_LB_DIGITS-1 go to table 0 (e·B),
+// the next SV_LB_DIGITS to table 1 (e·2^128 B), so the recoding carry out of
+// the low half flows into the high half and never needs a digit of its own
+// (16 base-point additions per signature at radix 2^16, was 18 when each half
+// was recoded separately).  Digit j of both halves is added at window
+// SV_LB_WIN * j.  Tables: e * 2^(128 t) * B for e in [0, 2^(SV_LB_BITS-1)].
+// (Radix 2^20, 151 MB of tables, measured no faster than radix 2^16 (9.4 MB,
+// L2/MALL-resident): the saved additions came back as exposed latency of the
+// DMA'd entries.)
 #ifndef SV_LB_BITS
 #define SV_LB_BITS 16
 #endif
+static_assert(SV_LB_BITS % 4 == 0 && 128 % SV_LB_BITS == 0 && SV_LB_BITS <= 16, "base-point digit radix");
 #define SV_LB_WIN (SV_LB_BITS / 4)
-#define SV_LB_DIGITS ((128 + SV_LB_BITS) / SV_LB_BITS)
+#define SV_LB_DIGITS (128 / SV_LB_BITS)
 #define SV_LBTAB_ENTRIES ((1 << (SV_LB_BITS - 1)) + 1)
 
 SV_HD void sv_btab_entry_shift(uint32_t out[SV_BTAB_STRIDE], int e, int shift) {
@@ -571,8 +576,9 @@ SV_HD void sv_digits_shift(uint32_t d[8], int k) {
 
 // Per-signature digit strings of (*) in lattice.h for W windows:
 //   dA: c0, dR: |c1| (signed radix 16, top digit = window W-1),
-//   dB0[j], dB1[j] = signed radix-2^SV_LB_BITS digit j of (s mod 2^128) and of
-//   (s >> 128), s = c1 S mod L; digit j is added at window SV_LB_WIN * j.
+//   dB0[j], dB1[j] = signed radix-2^SV_LB_BITS digits j and SV_LB_DIGITS + j of
+//   s = c1 S mod L (one string, sc_digits_lb); both are added at window
+//   SV_LB_WIN * j, from the tables e·B and e·2^128 B.
 // A scalar of 4W-1 bits can carry out of digit W-1: that digit is then -8 and
 // the carry is 1, i.e. the top digit is really +8 (table entries go to 8);
 // top8A / top8R record it (4-bit two's complement digits stop at 7).
@@ -582,16 +588,19 @@ struct sv_lat_digits {
   bool rneg, top8A, top8R;
 };
 
-// Signed radix-2^SV_LB_BITS digits of a 128-bit x: d_j in [-2^(B-1), 2^(B-1)).
-SV_HD void sc_digits_lb(int32_t d[SV_LB_DIGITS], const uint32_t x[4]) {
+// Signed radix-2^SV_LB_BITS digits of x < 2^253 (8 words), as one string:
+// d0 = digits 0..SV_LB_DIGITS-1 (weights 2^(B j)), d1 = the next SV_LB_DIGITS
+// (weights 2^128 2^(B j)); every digit in [-2^(B-1), 2^(B-1)).  The top digit
+// is < 2^(253-256+B) + 1 <= 2^(B-1), so no carry is left over.
+SV_HD void sc_digits_lb(int32_t d0[SV_LB_DIGITS], int32_t d1[SV_LB_DIGITS], const uint32_t x[8]) {
   uint32_t carry = 0;
-  SV_UNROLL for (int j = 0; j < SV_LB_DIGITS; ++j) {
-    const int o = j * SV_LB_BITS, q = o >> 5, r = o & 31;
-    uint32_t v = q < 4 ? (x[q] >> r) : 0u;
-    if (r != 0 && q + 1 < 4 && r + SV_LB_BITS > 32) v |= x[q + 1] << (32 - r);
-    v = (v & ((1u << SV_LB_BITS) - 1u)) + carry;
+  SV_UNROLL for (int j = 0; j < 2 * SV_LB_DIGITS; ++j) {
+    const int o = j * SV_LB_BITS, q = o >> 5, r = o & 31;  // (B divides 32: never straddles a word)
+    uint32_t v = ((x[q] >> r) & ((1u << SV_LB_BITS) - 1u)) + carry;
     carry = (v + (1u << (SV_LB_BITS - 1))) >> SV_LB_BITS;  // v >= 2^(B-1)
-    d[j] = (int32_t)v - (int32_t)(carry << SV_LB_BITS);
+    const int32_t d = (int32_t)v - (int32_t)(carry << SV_LB_BITS);
+    if (j < SV_LB_DIGITS) d0[j] = d;
+    else d1[j - SV_LB_DIGITS] = d;
   }
 }
 
@@ -624,8 +633,7 @@ SV_COLD void sv_lat_prepare(sv_lat_digits& D, const sv_lat& lat, const uint32_t 
   D.rneg = lat.c1neg;
   uint32_t s[8];
   sc_mul_signed(s, lat.c1, lat.c1neg, S);
-  sc_digits_lb(D.dB0, s);      // s mod 2^128
-  sc_digits_lb(D.dB1, s + 4);  // s >> 128 (< 2^125)
+  sc_digits_lb(D.dB0, D.dB1, s);  // s < L: low / high 128-bit halves, one carry chain
 }
 
 // 1: one 10-quad stage region per wave instead of two (10 KB): each entry is
@@ -653,7 +661,7 @@ SV_HD void sv_stage_lentry(sv_u4* stage, const sv_u4* entry) {
 // the lane's tables of -A / -R; btab0 / btab1: e·B / e·(2^128 B).
 // Step machine per window w: s = 0..3 doubling (skipped in the top window,
 // where P is the identity), s = 4 add tabA[dA], s = 5 add tabR[+-dR], and on
-// windows w = 4j, j <= 8: s = 6 add btab0[dB0_j], s = 7 add btab1[dB1_j].
+// windows w = 4j, j < SV_LB_DIGITS: s = 6 add btab0[dB0_j], s = 7 add btab1[dB1_j].
 // STAGED (device): the window's A and R entries are DMA'd into the wave's LDS
 // stage (2 x 10 quads x 64 lanes) when the window starts.
 template <bool STAGED = false>
