@@ -88,11 +88,17 @@ typedef struct svh_mb_stats {
   uint64_t items, batches, flushed_by_size, flushed_by_deadline, max_batch;
   double lat_p50_us, lat_p99_us; /* submit -> verdict ready */
 } svh_mb_stats;
-/* Feed n signatures through a VerifyMicroBatcher from `producers` threads
- * (item i from thread i % producers, optional sleep between submissions). */
+/* Feed n signatures through a VerifyMicroBatcher (2 flush workers) from
+ * `producers` threads (item i from thread i % producers, optional sleep
+ * between submissions). */
 int svh_mb_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                const uint32_t* msg_len, size_t n, int producers, uint32_t max_batch, uint32_t max_delay_us,
                uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats);
+/* Same with `workers` flush threads (VerifyMicroBatcher workers > 1: several
+ * batches in flight, host work of one overlapping the engine call of another). */
+int svh_mb_run_workers(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                       const uint32_t* msg_len, size_t n, int producers, int workers, uint32_t max_batch,
+                       uint32_t max_delay_us, uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats);
 
 #ifdef __cplusplus
 }

@@ -6,8 +6,12 @@
 
 namespace stellar {
 
-VerifyMicroBatcher::VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay)
-    : mMaxBatch(std::max<size_t>(1, maxBatch)), mMaxDelay(maxDelay), mWorker([this] { run(); }) {}
+VerifyMicroBatcher::VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay, unsigned workers)
+    : mMaxBatch(std::max<size_t>(1, maxBatch)), mMaxDelay(maxDelay) {
+  const unsigned w = std::max(1u, workers);
+  mWorkers.reserve(w);
+  for (unsigned i = 0; i < w; ++i) mWorkers.emplace_back([this] { run(); });
+}
 
 VerifyMicroBatcher::~VerifyMicroBatcher() {
   {
@@ -15,7 +19,7 @@ VerifyMicroBatcher::~VerifyMicroBatcher() {
     mStop = true;
   }
   mCv.notify_all();
-  mWorker.join();
+  for (auto& w : mWorkers) w.join();
 }
 
 std::future<bool> VerifyMicroBatcher::submit(PublicKey const& key, Signature const& sig, ByteSlice const& msg) {
@@ -51,13 +55,15 @@ void VerifyMicroBatcher::run() {
   for (;;) {
     // wait for: stop, a full batch, or the oldest item's deadline
     while (!mStop && mQueue.empty()) mCv.wait(lk);
-    if (mQueue.empty() && mStop) return;
-    bool bySize = mQueue.size() >= mMaxBatch;
-    if (!bySize && !mStop) {
+    if (mQueue.empty()) return;  // stop requested and the queue is drained
+    if (mQueue.size() < mMaxBatch && !mStop) {
       const auto deadline = mQueue.front().t0 + mMaxDelay;
-      mCv.wait_until(lk, deadline, [&] { return mStop || mQueue.size() >= mMaxBatch; });
-      bySize = mQueue.size() >= mMaxBatch;
+      if (std::chrono::steady_clock::now() < deadline) {
+        mCv.wait_until(lk, deadline, [&] { return mStop || mQueue.size() >= mMaxBatch; });
+        continue;  // re-evaluate: another worker may have taken the queue meanwhile
+      }
     }
+    const bool bySize = mQueue.size() >= mMaxBatch;
     const size_t take = std::min(mQueue.size(), mMaxBatch);
     std::vector<Item> batch;
     batch.reserve(take);
@@ -69,6 +75,7 @@ void VerifyMicroBatcher::run() {
     if (bySize) ++mStats.flushedBySize;
     else ++mStats.flushedByDeadline;
     mStats.maxBatchSeen = std::max<uint64_t>(mStats.maxBatchSeen, take);
+    if (!mQueue.empty()) mCv.notify_one();  // leftovers: another worker can take them
     lk.unlock();
     std::vector<PubKeyUtils::VerifyItem> items;
     items.reserve(take);

@@ -135,14 +135,15 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
   }
 }
 
-int svh_mb_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
-               const uint32_t* msg_len, size_t n, int producers, uint32_t max_batch, uint32_t max_delay_us,
-               uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats) {
+int svh_mb_run_workers(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                       const uint32_t* msg_len, size_t n, int producers, int workers, uint32_t max_batch,
+                       uint32_t max_delay_us, uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats) {
   try {
     if (producers < 1) producers = 1;
+    if (workers < 1) workers = 1;
     std::vector<int> err(producers, 0);
     std::vector<std::string> msgs(producers);
-    VerifyMicroBatcher mb(max_batch, std::chrono::microseconds(max_delay_us));
+    VerifyMicroBatcher mb(max_batch, std::chrono::microseconds(max_delay_us), (unsigned)workers);
     std::vector<std::thread> th;
     for (int p = 0; p < producers; ++p) {
       th.emplace_back([&, p] {
@@ -184,6 +185,13 @@ int svh_mb_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const 
   } catch (std::exception const& e) {
     return guard_exc(e);
   }
+}
+
+int svh_mb_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+               const uint32_t* msg_len, size_t n, int producers, uint32_t max_batch, uint32_t max_delay_us,
+               uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats) {
+  return svh_mb_run_workers(pk, sig, msg, msg_off, msg_len, n, producers, 2, max_batch, max_delay_us,
+                            inter_arrival_us, verdict, stats);
 }
 
 }  // extern "C"

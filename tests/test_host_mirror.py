@@ -289,7 +289,7 @@ class MbStats(ctypes.Structure):
                 ("lat_p50_us", ctypes.c_double), ("lat_p99_us", ctypes.c_double)]
 
 
-def _mb_run(host, d, rows, producers, max_batch, max_delay_us, gap_us=0):
+def _mb_run(host, d, rows, producers, max_batch, max_delay_us, gap_us=0, workers=1):
     n = len(rows)
     pk = np.ascontiguousarray(d["pk"][rows])
     sig = np.ascontiguousarray(d["sig"][rows])
@@ -299,10 +299,16 @@ def _mb_run(host, d, rows, producers, max_batch, max_delay_us, gap_us=0):
     out = np.full(n, 7, np.uint8)
     st = MbStats()
     vp = ctypes.c_void_p
-    rc = host.svh_mb_run(vp(pk.ctypes.data), vp(sig.ctypes.data), vp(msg.ctypes.data), vp(off.ctypes.data),
-                         vp(ln.ctypes.data), ctypes.c_size_t(n), producers, ctypes.c_uint32(max_batch),
-                         ctypes.c_uint32(max_delay_us), ctypes.c_uint32(gap_us), vp(out.ctypes.data),
-                         ctypes.byref(st))
+    if workers == 1:
+        rc = host.svh_mb_run(vp(pk.ctypes.data), vp(sig.ctypes.data), vp(msg.ctypes.data), vp(off.ctypes.data),
+                             vp(ln.ctypes.data), ctypes.c_size_t(n), producers, ctypes.c_uint32(max_batch),
+                             ctypes.c_uint32(max_delay_us), ctypes.c_uint32(gap_us), vp(out.ctypes.data),
+                             ctypes.byref(st))
+    else:
+        rc = host.svh_mb_run_workers(vp(pk.ctypes.data), vp(sig.ctypes.data), vp(msg.ctypes.data),
+                                     vp(off.ctypes.data), vp(ln.ctypes.data), ctypes.c_size_t(n), producers, workers,
+                                     ctypes.c_uint32(max_batch), ctypes.c_uint32(max_delay_us),
+                                     ctypes.c_uint32(gap_us), vp(out.ctypes.data), ctypes.byref(st))
     assert rc == 0, host.svh_last_error_string()
     return out, st
 
@@ -328,6 +334,23 @@ def test_micro_batcher_deadline_flush(host, engine, golden):
     assert (out == 1).all()
     assert st.flushed_by_size == 0 and st.flushed_by_deadline >= 1
     assert st.lat_p99_us >= 0 and st.items == 5
+
+
+def test_micro_batcher_multiple_workers(host, engine, golden):
+    """Several flush workers (batches in flight at once): same verdicts, every
+    item in exactly one batch, size and deadline flushes both still honoured."""
+    d = golden["adversarial"]
+    rows = np.arange(0, len(d["verdict"]), 3)
+    out, st = _mb_run(host, d, rows, producers=6, max_batch=16, max_delay_us=100_000, workers=3)
+    assert (out == d["verdict"][rows]).all()
+    assert st.items == len(rows) and st.max_batch <= 16
+    assert st.batches >= (len(rows) + 15) // 16 and st.flushed_by_size >= 1
+    assert st.batches == st.flushed_by_size + st.flushed_by_deadline
+    d = golden["valid"]
+    rows = np.arange(6)
+    out, st = _mb_run(host, d, rows, producers=1, max_batch=1000, max_delay_us=3000, gap_us=500, workers=3)
+    assert (out == 1).all()
+    assert st.flushed_by_size == 0 and st.flushed_by_deadline >= 1 and st.items == 6
 
 
 @pytest.mark.gpu

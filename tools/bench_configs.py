@@ -322,15 +322,15 @@ def configmb(env, n=200_000, producers=8):
     want[::97] = 0
     vp = ctypes.c_void_p
 
-    def run(max_batch, max_delay_us):
+    def run(max_batch, max_delay_us, workers=1):
         out = np.zeros(n, np.uint8)
         st = MbStats()
         env.host.svh_cache_clear()
         t0 = time.perf_counter()
-        rc = env.host.svh_mb_run(vp(pk.ctypes.data), vp(sig.ctypes.data), vp(msg.ctypes.data), vp(off.ctypes.data),
-                                 vp(lens.ctypes.data), ctypes.c_size_t(n), producers, ctypes.c_uint32(max_batch),
-                                 ctypes.c_uint32(max_delay_us), ctypes.c_uint32(0), vp(out.ctypes.data),
-                                 ctypes.byref(st))
+        rc = env.host.svh_mb_run_workers(vp(pk.ctypes.data), vp(sig.ctypes.data), vp(msg.ctypes.data),
+                                         vp(off.ctypes.data), vp(lens.ctypes.data), ctypes.c_size_t(n), producers,
+                                         workers, ctypes.c_uint32(max_batch), ctypes.c_uint32(max_delay_us),
+                                         ctypes.c_uint32(0), vp(out.ctypes.data), ctypes.byref(st))
         dt = time.perf_counter() - t0
         assert rc == 0, env.host.svh_last_error_string()
         return {"verifies_per_s": n / dt, "batches": st.batches, "flushed_by_size": st.flushed_by_size,
@@ -341,6 +341,9 @@ def configmb(env, n=200_000, producers=8):
     res = {"messages": n, "producers": producers, "gpu": {}}
     for mbatch in (1024, 8192, 65536):
         res["gpu"]["max_batch_%d" % mbatch] = run(mbatch, 2000)
+    for workers in (2, 4, 8):  # several flush workers: batches in flight at once
+        for mbatch in (1024, 8192):
+            res["gpu"]["max_batch_%d_workers_%d" % (mbatch, workers)] = run(mbatch, 2000, workers)
     base = env.base
     base.cpubase_set_sodium.argtypes = [ctypes.c_char_p, ctypes.c_int]
     assert base.cpubase_set_sodium(SODIUM.encode(), 1) == 0
