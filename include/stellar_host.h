@@ -15,10 +15,25 @@
  *                              (/root/reference/src/transactions/SignatureChecker.cpp:30-158),
  *                              optionally after one GPU batch pre-pass over the
  *                              whole set
+ *   svh_check_envelopes     == the signature checks of TransactionFrame::checkValid /
+ *                              apply and FeeBumpTransactionFrame::checkValid over ONE
+ *                              checker per envelope: source account at LOW, extra
+ *                              signers, every operation at its threshold, all
+ *                              signatures used (TransactionFrame.cpp:268-321,
+ *                              1091-1156, 1185-1301, 1416-1486; OperationFrame.cpp:
+ *                              173-209; FeeBumpTransactionFrame.cpp:138-197), optionally
+ *                              after one batch pre-pass over every envelope (a tx set,
+ *                              f1, or a whole catchup checkpoint, f3: verdicts in a
+ *                              side table, the 0xffff cache bypassed)
  *   svh_mb_run              == VerifyMicroBatcher driven by `producers` threads: the
  *                              SCP/overlay pre-verify (/root/reference/src/overlay/
  *                              Peer.cpp:963-970) turned into size/deadline-flushed
  *                              GPU batches
+ *
+ * Nothing here reports an engine (GPU) error: the mirror re-runs a failed
+ * batch on the engine's CPU path (sv_ed25519_verify_batch_cpu), like the
+ * reference's verifySig, which never fails.  svh_engine_counts_ex reports how
+ * often that happened.
  */
 #ifndef STELLAR_HOST_H
 #define STELLAR_HOST_H
@@ -32,7 +47,7 @@ extern "C" {
 
 #define SVH_OK 0
 #define SVH_ERR_INVALID_ARG (-1)
-#define SVH_ERR_ENGINE (-2) /* device error: the batch is unverified, never rejected */
+#define SVH_ERR_ENGINE (-2) /* (kept for ABI stability; engine errors are absorbed by the CPU path) */
 
 typedef struct svh_signer {
   uint8_t type; /* 0 ED25519, 1 PRE_AUTH_TX, 2 HASH_X, 3 ED25519_SIGNED_PAYLOAD */
@@ -70,23 +85,81 @@ int svh_verify_sig_batch(const uint8_t* pk, const uint8_t* sig /* n x 64 */, con
 void svh_cache_clear(void);
 void svh_cache_seed(unsigned int seed);
 void svh_cache_counts(uint64_t* hits, uint64_t* misses); /* flushes, like flushVerifySigCacheCounts */
-void svh_engine_counts(uint64_t* signatures, uint64_t* batches);
+/* the cache's keys in its insertion-order vector (the reference's mValuePtrs);
+ * writes min(max_keys, size) keys of 32 bytes, returns the cache size */
+size_t svh_cache_keys(uint8_t* out, size_t max_keys);
+void svh_engine_counts(uint64_t* signatures, uint64_t* batches); /* GPU signatures / calls; flushes */
+typedef struct svh_engine_stats {
+  uint64_t gpu_signatures, gpu_batches, cpu_signatures, fallbacks;
+} svh_engine_stats;
+void svh_engine_counts_ex(svh_engine_stats* out); /* flushes all four */
+/* batches with at most max_misses cache misses run on the CPU path (default 1) */
+void svh_set_cpu_threshold(size_t max_misses);
+/* engine-only batch, no cache (PubKeyUtils::verifyBatchUncached) */
+int svh_verify_uncached(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                        const uint32_t* msg_len, size_t n, uint8_t* verdict);
 /* test hook: route cache misses to fn instead of the GPU (NULL restores) */
 void svh_set_test_verifier(svh_batch_verify_fn fn);
 /* Keyed batches: verifySigBatch calls with >= min_items
  * eligible signatures get verdicts AND BLAKE2b cache keys from one engine pass
- * (sv_ed25519_verify_batch_keyed); 0 disables; default 4096.  The keyed test
- * hook replaces that engine call (CPU tests). */
+ * (sv_ed25519_verify_batch_gather with keys); 0 disables; default 256.  The
+ * keyed test hook replaces that engine call (CPU tests). */
 typedef int (*svh_keyed_verify_fn)(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
                                    const uint32_t* len, size_t n, uint8_t* verdict, uint8_t* keys);
 void svh_set_test_keyed_verifier(svh_keyed_verify_fn fn);
 void svh_set_keyed_threshold(size_t min_items);
+/* use_prefetch: 0 none; 1 one batch pre-pass into a side table; 2 the same
+ * through verifySigBatch (also seeds the verify cache) */
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs);
 
+/* ---- transaction-level checks (a13) ---- */
+typedef struct svh_account {
+  uint8_t account_id[32];
+  uint8_t thresholds[4]; /* master weight, LOW, MEDIUM, HIGH */
+  uint32_t nsigners, signer_off; /* range in the svh_signer array */
+} svh_account;
+
+typedef struct svh_op {
+  uint8_t has_source; /* 0: the transaction's source account */
+  uint8_t level;      /* 1 LOW, 2 MEDIUM, 3 HIGH */
+  uint8_t source[32];
+  uint8_t pad[2];
+} svh_op;
+
+typedef struct svh_envelope {
+  uint8_t contents_hash[32]; /* of the (inner) transaction */
+  uint8_t source[32];
+  uint32_t nsigs, sig_off;   /* the transaction's signatures */
+  uint32_t nops, op_off;
+  uint32_t nextra, extra_off; /* extra signer keys (svh_signer, weight ignored) */
+  uint32_t fee_bump;          /* 1: fee-bump envelope around the transaction */
+  uint8_t fee_bump_hash[32];
+  uint8_t fee_source[32];
+  uint32_t nouter, outer_off; /* fee-bump (outer) signatures */
+} svh_envelope;
+
+typedef struct svh_tx_result {
+  int32_t code;       /* TransactionResultCode: 0 txSUCCESS, 1 txFEE_BUMP_INNER_SUCCESS, -1 txFAILED,
+                         -6 txBAD_AUTH, -8 txNO_ACCOUNT, -10 txBAD_AUTH_EXTRA, -12 txNOT_SUPPORTED,
+                         -13 txFEE_BUMP_INNER_FAILED */
+  int32_t inner_code; /* fee bump: the inner transaction's code */
+  int32_t failed_op;  /* txFAILED: the first failing operation, else -1 */
+  int32_t op_code;    /* 0 opINNER, -1 opBAD_AUTH, -2 opNO_ACCOUNT */
+} svh_tx_result;
+
+/* prefetch: 0 none, 1 side table (cache bypassed: the per-checkpoint catchup
+ * form), 2 side table + verify cache.  for_apply: 0 checkValid path, 1 apply
+ * path (processSignatures). */
+int svh_check_envelopes(const svh_envelope* env, size_t n, const svh_decorated_sig* sigs, const svh_op* ops,
+                        const svh_signer* signers, const svh_account* accounts, size_t naccounts,
+                        uint32_t protocol, int prefetch, int for_apply, svh_tx_result* results,
+                        uint64_t* prefetched_pairs);
+
 typedef struct svh_mb_stats {
   uint64_t items, batches, flushed_by_size, flushed_by_deadline, max_batch;
-  double lat_p50_us, lat_p99_us; /* submit -> verdict ready */
+  double lat_p50_us, lat_p99_us; /* submit -> verdict ready (submit mode) */
+  double wall_s;                 /* first submission -> last verdict */
 } svh_mb_stats;
 /* Feed n signatures through a VerifyMicroBatcher (2 flush workers) from
  * `producers` threads (item i from thread i % producers, optional sleep
@@ -96,6 +169,13 @@ int svh_mb_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const 
                uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats);
 /* Same with `workers` flush threads (VerifyMicroBatcher workers > 1: several
  * batches in flight, host work of one overlapping the engine call of another). */
+/* fire_and_forget: producers post() (verdicts only warm the verify cache, as the
+ * reference's pre-verify) instead of submit(); verdict[] is then read back
+ * from the cache after the run */
+int svh_mb_run_ex(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                  const uint32_t* msg_len, size_t n, int producers, int workers, uint32_t max_batch,
+                  uint32_t max_delay_us, uint32_t inter_arrival_us, int fire_and_forget, uint8_t* verdict,
+                  svh_mb_stats* stats);
 int svh_mb_run_workers(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                        const uint32_t* msg_len, size_t n, int producers, int workers, uint32_t max_batch,
                        uint32_t max_delay_us, uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats);

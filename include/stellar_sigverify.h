@@ -50,8 +50,9 @@ extern "C" {
 /* Batch options.  A NULL opts pointer means "all defaults". */
 typedef struct sv_opts {
   uint32_t struct_size; /* sizeof(sv_opts), for forward compatibility */
-  int32_t device;       /* -1 (default): shard contiguous slices over all devices; k >= 0: device k only */
-  uint32_t max_devices; /* 0 (default): no limit; else use at most this many devices when device == -1 */
+  int32_t device;       /* -1 (default): contiguous slices over the device slots, every slice at least the
+                           minimum shard (sv_set_min_shard; smaller batches run on one slot); k >= 0: slot k only */
+  uint32_t max_devices; /* 0 (default): no limit; else use at most this many slots when device == -1 */
   uint32_t flags;       /* 0 or one SV_FLAG_PATH_* (kernel path for this call); other bits must be 0 */
 } sv_opts;
 
@@ -72,9 +73,19 @@ typedef struct sv_opts {
  * API never does).  Returns the previous default, or SV_ERR_INVALID_ARG. */
 int sv_set_kernel_path(int path);
 
-/* Initialise every visible device (B-table, workspace, streams).  Idempotent.
- * Called implicitly by the verify entry points. */
+/* Enumerate the device slots (one per visible GPU unless a device map says
+ * otherwise).  Idempotent; called implicitly by every entry point.  Per-slot
+ * resources (streams, base-point tables, workspace, pinned staging) are
+ * created on the slot's first use; the throughput-path workspace is sized to
+ * the batch and grows on demand. */
 int sv_init(void);
+/* Device slots -> physical GPUs, e.g. {0, 0}: two logical slots on GPU 0
+ * (tests of the multi-device path on one GPU).  Releases every slot's
+ * resources first; count == 0 restores one slot per visible GPU.  The
+ * environment variable SV_DEVICE_MAP="0,0" sets the same at first init. */
+int sv_set_device_map(const int* physical, int count);
+/* Minimum signatures per slot when a batch is sharded (default 65536). */
+int sv_set_min_shard(size_t n);
 /* Release all device resources.  Safe to call more than once. */
 void sv_shutdown(void);
 /* Number of usable devices (initialises on first use); negative on error. */
@@ -94,6 +105,32 @@ const char* sv_version(void);
 int sv_ed25519_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                             const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
                             uint8_t* verdict, const sv_opts* opts);
+
+/*
+ * Gather form of sv_ed25519_verify_batch: item i is (pk[i] -> 32 bytes,
+ * sig[i] -> 64 bytes, msg[i] -> msg_len[i] bytes), packed by the engine
+ * straight into its pinned staging (no intermediate copy by the caller, e.g.
+ * PubKeyUtils::verifySigBatch over VerifyItem pointers).  keys (optional, n x
+ * 32) also receives each item's verify-cache key BLAKE2b-256(pk || sig ||
+ * msg) from the same staging (SecretKey.cpp:50-61).
+ */
+int sv_ed25519_verify_batch_gather(const uint8_t* const* pk, const uint8_t* const* sig, const uint8_t* const* msg,
+                                   const uint32_t* msg_len, size_t n, uint8_t* verdict, uint8_t* keys,
+                                   const sv_opts* opts);
+
+/*
+ * CPU path: the engine's own per-signature algorithm (csrc/verify_core.h,
+ * the half-size equation of csrc/lattice.h) compiled for the host, on
+ * `threads` threads (0: the machine's hardware concurrency, capped at 16).
+ * Same verdicts as every GPU path.  It is what a caller runs when a GPU entry
+ * point returns an error (an error is never a reject) and what the C++ mirror
+ * uses for single-signature verifySig calls, where a GPU round trip costs more
+ * than the verification itself.  Message layout as in sv_ed25519_verify_batch.
+ */
+int sv_ed25519_verify_batch_cpu(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                                const uint32_t* msg_len, size_t n, uint8_t* verdict, int threads);
+/* single-signature form (returns 1 valid, 0 invalid) */
+int sv_ed25519_verify_cpu(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, size_t msg_len);
 
 /*
  * Fixed-length batch, host buffers: message i = msg[i*msg_len .. (i+1)*msg_len).
@@ -158,6 +195,20 @@ int sv_verify_cache_keys_device(int device, const void* d_pk, const void* d_sig,
                                 size_t n, void* d_keys, void* stream);
 int sv_sha256_device(int device, const void* d_data, const uint64_t* d_off, const uint32_t* d_len,
                      uint32_t fixed_len, size_t n, void* d_digests, void* stream);
+
+/* Test knobs (0 in production).  TRIVIAL_PAIR: every lane verifies through the
+ * fallback pair (h, 1) of the half-size equation (lattice.h), i.e. the
+ * full-length scalar; MAX_WINDOWS: every wave runs all 64 windows; FAIL: every
+ * GPU entry point returns SV_ERR_HIP without touching the device (callers'
+ * CPU fallback tests).  Returns the previous flags, or SV_ERR_INVALID_ARG. */
+#define SV_DBG_TRIVIAL_PAIR 0x1u
+#define SV_DBG_MAX_WINDOWS 0x2u
+#define SV_DBG_FAIL 0x4u
+int sv_set_debug_flags(uint32_t flags);
+
+/* Bytes of the slot's kernel workspace / pinned staging currently allocated. */
+int sv_workspace_bytes(int device, size_t* bytes);
+int sv_pinned_bytes(int device, size_t* bytes);
 
 /* Kernel-time accounting for profiling: when enabled, every verify launch is
  * bracketed by HIP events on the device's internal stream and the elapsed

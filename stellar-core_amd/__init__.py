@@ -62,7 +62,12 @@ EXPORTED_SYMBOLS = (
     "sv_ed25519_sign_device", "sv_timing_enable", "sv_kernel_time", "sv_kernel_time_reset",
     "sv_device_synchronize", "sv_verify_cache_keys", "sv_ed25519_verify_batch_keyed", "sv_sha256_batch",
     "sv_verify_cache_keys_device", "sv_sha256_device", "sv_set_kernel_path",
+    "sv_ed25519_verify_batch_gather", "sv_ed25519_verify_batch_cpu", "sv_ed25519_verify_cpu",
+    "sv_set_device_map", "sv_set_min_shard", "sv_set_debug_flags", "sv_workspace_bytes", "sv_pinned_bytes",
 )
+
+# test knobs (include/stellar_sigverify.h sv_set_debug_flags)
+DBG_TRIVIAL_PAIR, DBG_MAX_WINDOWS, DBG_FAIL = 0x1, 0x2, 0x4
 
 
 class SigVerifyError(RuntimeError):
@@ -117,6 +122,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sv_sha256_batch.argtypes = [vp, vp, vp, sz, vp, vp]
     lib.sv_verify_cache_keys_device.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_uint32, sz, vp, vp]
     lib.sv_sha256_device.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, sz, vp, vp]
+    lib.sv_ed25519_verify_batch_gather.argtypes = [vp, vp, vp, vp, sz, vp, vp, vp]
+    lib.sv_ed25519_verify_batch_cpu.argtypes = [vp, vp, vp, vp, vp, sz, vp, ctypes.c_int]
+    lib.sv_ed25519_verify_cpu.argtypes = [vp, vp, vp, sz]
+    lib.sv_set_device_map.argtypes = [vp, ctypes.c_int]
+    lib.sv_set_min_shard.argtypes = [sz]
+    lib.sv_set_debug_flags.argtypes = [ctypes.c_uint32]
+    lib.sv_workspace_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
+    lib.sv_pinned_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
     _lib = lib
     return lib
 
@@ -273,6 +286,67 @@ def verify_device(device: int, d_pk: int, d_sig: int, d_msg: int, n: int, d_verd
 def sign_device(device: int, d_seed: int, d_msg32: int, n: int, d_pk: int, d_sig: int, stream: int = 0) -> None:
     lib = load_library()
     _check(lib.sv_ed25519_sign_device(device, d_seed, d_msg32, n, d_pk, d_sig, stream or None))
+
+
+def verify_batch_cpu(pk, sig, msg, msg_off, msg_len, threads: int = 0) -> np.ndarray:
+    """The engine's CPU path (same algorithm, host build): what a caller runs
+    when a GPU entry point fails, and what single verifySig calls use."""
+    lib = load_library()
+    pk, sig = _u8(pk, 32), _u8(sig, 64)
+    n = pk.shape[0]
+    msg, off, ln = _var_msgs(msg, msg_off, msg_len, n)
+    out = np.zeros(n, np.uint8)
+    _check(lib.sv_ed25519_verify_batch_cpu(_ptr(pk), _ptr(sig), _ptr(msg), _ptr(off), _ptr(ln), n, _ptr(out),
+                                           int(threads)))
+    return out
+
+
+def verify_gather(items, keys: bool = False, device: int = -1, max_devices: int = 0):
+    """Gather form: items = [(pk32, sig64, msg), ...] as bytes objects; the engine
+    packs them straight from their buffers.  Returns verdicts (and cache keys)."""
+    lib = load_library()
+    n = len(items)
+    bufs = [(bytes(p), bytes(s), bytes(m)) for p, s, m in items]
+    P = (ctypes.c_char_p * max(1, n))(*[b[0] for b in bufs])
+    S = (ctypes.c_char_p * max(1, n))(*[b[1] for b in bufs])
+    M = (ctypes.c_char_p * max(1, n))(*[b[2] for b in bufs])
+    L = np.array([len(b[2]) for b in bufs], np.uint32)
+    out = np.zeros(n, np.uint8)
+    kb = np.zeros((n, 32), np.uint8) if keys else None
+    _check(lib.sv_ed25519_verify_batch_gather(ctypes.cast(P, ctypes.c_void_p), ctypes.cast(S, ctypes.c_void_p),
+                                              ctypes.cast(M, ctypes.c_void_p), _ptr(L), n, _ptr(out),
+                                              _ptr(kb) if keys else None, _opts(device, max_devices)))
+    return (out, kb) if keys else out
+
+
+def set_device_map(physical) -> None:
+    """Device slots -> physical GPUs (e.g. [0, 0]: two slots on GPU 0); [] restores."""
+    lib = load_library()
+    arr = (ctypes.c_int * max(1, len(physical)))(*physical)
+    _check(lib.sv_set_device_map(ctypes.cast(arr, ctypes.c_void_p), len(physical)))
+
+
+def set_min_shard(n: int) -> None:
+    _check(load_library().sv_set_min_shard(int(n)))
+
+
+def set_debug_flags(flags: int) -> int:
+    rc = load_library().sv_set_debug_flags(int(flags))
+    if rc < 0:
+        _check(rc)
+    return rc
+
+
+def workspace_bytes(device: int = 0) -> int:
+    v = ctypes.c_size_t()
+    _check(load_library().sv_workspace_bytes(device, ctypes.byref(v)))
+    return v.value
+
+
+def pinned_bytes(device: int = 0) -> int:
+    v = ctypes.c_size_t()
+    _check(load_library().sv_pinned_bytes(device, ctypes.byref(v)))
+    return v.value
 
 
 def set_kernel_path(path: int) -> int:

@@ -1,21 +1,106 @@
 // See PubKeyUtils.h.  Reference: /root/reference/src/crypto/SecretKey.cpp:37-61
 // (cache + key), :317-339 (cache control), :435-468 (verifySig);
-// /root/reference/src/util/RandomEvictionCache.h:20-245 (the cache).
+// /root/reference/src/util/RandomEvictionCache.h:20-245 (the cache);
+// /root/reference/lib/util/stdrandom.h (the pinned uniform_int_distribution).
 #include "PubKeyUtils.h"
 
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <random>
 #include <string>
 
 #include "../../../include/stellar_sigverify.h"
+#include "../pool.h"
 #include "hashes.h"
 
 namespace stellar {
 namespace {
 
+sv::Pool& hostPool() {
+  static sv::Pool p(std::min(8u, std::max(2u, std::thread::hardware_concurrency())));
+  return p;
+}
+
+// Runs fn(i) for i in [0, n) over up to `maxParts` pool tasks (serially for
+// small n).
+template <class F>
+void parallelFor(size_t n, size_t grain, F fn) {
+  const size_t parts = std::max<size_t>(1, std::min<size_t>(hostPool().size() + 1, n / std::max<size_t>(1, grain)));
+  if (parts == 1) {
+    for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  hostPool().run(parts, [&](size_t t) {
+    const size_t a = n * t / parts, b = n * (t + 1) / parts;
+    for (size_t i = a; i < b; ++i) fn(i);
+  });
+}
+
+// uniform_int_distribution<size_t>(lo, hi)(g) exactly as libc++ computes it
+// (the algorithm stellar-core pins in lib/util/stdrandom.h so results do not
+// vary between standard libraries), for std::minstd_rand -- the reference's
+// stellar_default_random_engine (src/util/Math.h:26), whose result_type is a
+// 64-bit unsigned long on this ABI.  The draw builds a w-bit number (w =
+// bits of the range) from engine outputs: n outputs of w0 bits (n0 of them)
+// or w0 + 1 bits, each rejection-sampled below the largest multiple of 2^w0
+// (2^(w0+1)) within the engine range, and the whole is rejected while >= the
+// range.
+size_t uniformIndex(std::minstd_rand& g, size_t lo, size_t hi) {
+  using U = uint64_t;
+  const U r = (U)hi - (U)lo + 1;
+  if (r == 1) return lo;
+  const size_t Dt = 64;
+  size_t w;
+  if (r == 0) {
+    w = Dt;
+  } else {
+    w = Dt - (size_t)__builtin_clzll(r) - 1;
+    if ((r & (std::numeric_limits<U>::max() >> (Dt - w))) != 0) ++w;
+  }
+  const U R = (U)std::minstd_rand::max() - (U)std::minstd_rand::min() + 1;  // 2^31 - 2
+  const size_t m = 63 - (size_t)__builtin_clzll(R);                        // floor(log2 R) = 30
+  size_t n = w / m + (w % m != 0);
+  size_t w0 = w / n;
+  U y0 = w0 < Dt ? (R >> w0) << w0 : 0;
+  if (R - y0 > y0 / n) {
+    ++n;
+    w0 = w / n;
+    y0 = w0 < Dt ? (R >> w0) << w0 : 0;
+  }
+  const size_t n0 = n - w % n;
+  const U y1 = w0 < Dt - 1 ? (R >> (w0 + 1)) << (w0 + 1) : 0;
+  const U mask0 = w0 > 0 ? ~U(0) >> (Dt - w0) : U(0);
+  const U mask1 = w0 < Dt - 1 ? ~U(0) >> (Dt - (w0 + 1)) : ~U(0);
+  auto bits = [&]() -> U {
+    U s = 0;
+    for (size_t k = 0; k < n0; ++k) {
+      U u;
+      do {
+        u = (U)g() - (U)std::minstd_rand::min();
+      } while (u >= y0);
+      s = w0 < Dt ? (s << w0) : 0;
+      s += u & mask0;
+    }
+    for (size_t k = n0; k < n; ++k) {
+      U u;
+      do {
+        u = (U)g() - (U)std::minstd_rand::min();
+      } while (u >= y1);
+      s = w0 < Dt - 1 ? (s << (w0 + 1)) : 0;
+      s += u & mask1;
+    }
+    return s;
+  };
+  if (r == 0) return (size_t)bits();
+  U u;
+  do {
+    u = bits();
+  } while (u >= r);
+  return (size_t)(u + lo);
+}
 
 inline uint64_t keyBits(Hash const& h) {
   uint64_t v;
@@ -25,15 +110,31 @@ inline uint64_t keyBits(Hash const& h) {
 
 // Restatement of RandomEvictionCache<Hash, bool>(maxSize, separatePRNG=true):
 // entries plus a vector of entry references in insertion order (the
-// reference's mValuePtrs); when over capacity, pick two positions of that
-// vector uniformly at random, evict the less recently accessed entry and
-// swap-remove its position -- the same draws and the same victims as the
-// reference.  The key -> entry index is a flat linear-probing table
-// (backward-shift deletion) instead of a node-based map: no allocation per
-// insert/evict, which keeps large verifySigBatch calls from being bound by
-// the allocator.
+// reference's mValuePtrs); when over capacity, draw two positions of that
+// vector (uniformIndex above, the reference's rand_uniform), evict the less
+// recently accessed entry and swap-remove its position.  get() and put() bump
+// a generation counter exactly as maybeGet()/put() do.  The key -> entry index
+// is a flat linear-probing table (backward-shift deletion) instead of a node
+// map: no allocation per insert/evict.  A slot holds the key's low 32 bits
+// (its home position and a tag that settles almost every mismatch) and the
+// entry id.
+//
+// Pending entries: a non-keyed verifySigBatch inserts its misses in item
+// order BEFORE verifying them (the value is filled in afterwards), so the
+// draws, generations and victims are those of sequential verifySig calls.  A
+// pending entry of another batch reads as a miss (that caller verifies and
+// puts it itself, as concurrent verifySig calls would).
 class RandomEvictionCache {
  public:
+  static constexpr uint32_t kNone = 0xffffffffu;
+  struct Entry {
+    Hash key;
+    uint64_t lastAccess;
+    uint64_t owner;  // != 0: pending, value not known yet (batch id)
+    uint32_t pendIdx;
+    bool value;
+  };
+
   explicit RandomEvictionCache(size_t maxSize) : maxSize_(maxSize) {
     size_t cap = 16;
     while (cap < 2 * (maxSize + 1)) cap <<= 1;
@@ -43,34 +144,56 @@ class RandomEvictionCache {
     order_.reserve(maxSize + 1);
   }
   void maybeSeed(unsigned seed) { rng_.seed(seed); }
-  // Hint for a lookup a few items ahead (memory-level parallelism).
   void prefetch(Hash const& k) const { __builtin_prefetch(&table_[keyBits(k) & mask_]); }
-  bool exists(Hash const& k) const { return find(k) != kNone; }
-  bool get(Hash const& k) {
-    Entry& e = entries_[find(k)];
-    e.lastAccess = ++generation_;
-    return e.value;
+  uint32_t find(Hash const& k) const {
+    const uint64_t tag = keyBits(k) & 0xffffffffu;
+    for (size_t s = tag & mask_;; s = (s + 1) & mask_) {
+      const uint64_t t = table_[s];
+      if (t == 0) return kNone;
+      if ((t >> 32) == tag && entries_[(uint32_t)t - 1].key == k) return (uint32_t)t - 1;
+    }
   }
-  void put(Hash const& k, bool v) {
+  Entry& at(uint32_t id) { return entries_[id]; }
+  // maybeGet() on a found entry
+  Entry& touch(uint32_t id) {
+    Entry& e = entries_[id];
+    e.lastAccess = ++generation_;
+    return e;
+  }
+  // put(); owner != 0 inserts a pending value
+  void put(Hash const& k, bool v, uint64_t owner = 0, uint32_t pendIdx = 0) {
     ++generation_;
     const uint32_t id = find(k);
     if (id != kNone) {
-      entries_[id].lastAccess = generation_;
-      entries_[id].value = v;
+      Entry& e = entries_[id];
+      e.lastAccess = generation_;
+      e.value = v;
+      e.owner = owner;
+      e.pendIdx = pendIdx;
       return;
     }
     uint32_t nid;
     if (!freeIds_.empty()) {
       nid = freeIds_.back();
       freeIds_.pop_back();
-      entries_[nid] = Entry{k, generation_, v};
+      entries_[nid] = Entry{k, generation_, owner, pendIdx, v};
     } else {
       nid = (uint32_t)entries_.size();
-      entries_.push_back(Entry{k, generation_, v});
+      entries_.push_back(Entry{k, generation_, owner, pendIdx, v});
     }
     insertSlot(k, nid);
     order_.push_back(nid);
     if (order_.size() > maxSize_) evictOne();
+  }
+  // fills in a pending value if the entry is still this batch's
+  void resolve(Hash const& k, uint64_t owner, uint32_t pendIdx, bool v) {
+    const uint32_t id = find(k);
+    if (id == kNone) return;
+    Entry& e = entries_[id];
+    if (e.owner == owner && e.pendIdx == pendIdx) {
+      e.value = v;
+      e.owner = 0;
+    }
   }
   void clear() {
     std::fill(table_.begin(), table_.end(), 0u);
@@ -79,37 +202,28 @@ class RandomEvictionCache {
     order_.clear();
   }
   size_t size() const { return order_.size(); }
+  std::vector<Hash> keysInOrder() const {
+    std::vector<Hash> out;
+    out.reserve(order_.size());
+    for (uint32_t id : order_) out.push_back(entries_[id].key);
+    return out;
+  }
 
  private:
-  static constexpr uint32_t kNone = 0xffffffffu;
-  struct Entry {
-    Hash key;
-    uint64_t lastAccess;
-    bool value;
-  };
-  // slot = (tag << 32) | (entry id + 1), 0 = empty; the tag (key bits 32..63)
-  // settles almost every mismatch without touching the entry slab
-  static uint64_t tagOf(Hash const& k) { return keyBits(k) >> 32; }
-  uint32_t find(Hash const& k) const {
-    const uint64_t tag = tagOf(k);
-    for (size_t s = keyBits(k) & mask_;; s = (s + 1) & mask_) {
-      const uint64_t t = table_[s];
-      if (t == 0) return kNone;
-      if ((t >> 32) == tag && entries_[(uint32_t)t - 1].key == k) return (uint32_t)t - 1;
-    }
-  }
   void insertSlot(Hash const& k, uint32_t id) {
-    size_t s = keyBits(k) & mask_;
+    const uint64_t tag = keyBits(k) & 0xffffffffu;
+    size_t s = tag & mask_;
     while (table_[s] != 0) s = (s + 1) & mask_;
-    table_[s] = (tagOf(k) << 32) | (uint64_t)(id + 1);
+    table_[s] = (tag << 32) | (uint64_t)(id + 1);
   }
   void eraseSlot(Hash const& k, uint32_t id) {
     size_t s = keyBits(k) & mask_;
     while ((uint32_t)table_[s] != id + 1) s = (s + 1) & mask_;
-    // backward-shift deletion keeps every probe chain intact
+    // backward-shift deletion keeps every probe chain intact (the home slot
+    // of an occupant is its tag & mask: no entry access needed)
     size_t hole = s;
     for (size_t j = (hole + 1) & mask_; table_[j] != 0; j = (j + 1) & mask_) {
-      const size_t home = keyBits(entries_[(uint32_t)table_[j] - 1].key) & mask_;
+      const size_t home = (size_t)(table_[j] >> 32) & mask_;
       if (((j - home) & mask_) >= ((j - hole) & mask_)) {
         table_[hole] = table_[j];
         hole = j;
@@ -120,9 +234,8 @@ class RandomEvictionCache {
   void evictOne() {
     const size_t sz = order_.size();
     if (sz == 0) return;
-    std::uniform_int_distribution<size_t> dist(0, sz - 1);
-    const size_t ia = dist(rng_);
-    const size_t ib = dist(rng_);
+    const size_t ia = uniformIndex(rng_, 0, sz - 1);
+    const size_t ib = uniformIndex(rng_, 0, sz - 1);
     const size_t iv = entries_[order_[ia]].lastAccess < entries_[order_[ib]].lastAccess ? ia : ib;
     const uint32_t victim = order_[iv];
     eraseSlot(entries_[victim].key, victim);
@@ -140,44 +253,96 @@ class RandomEvictionCache {
   std::minstd_rand rng_;  // stellar_default_random_engine, src/util/Math.h:26
 };
 
-// First occurrence of each key inside one batch (flat linear probing).
-class BatchFirstIndex {
- public:
-  static constexpr uint32_t kNone = 0xffffffffu;
-  explicit BatchFirstIndex(size_t n) {
-    size_t cap = 16;
-    while (cap < 2 * n + 2) cap <<= 1;
-    slot_.assign(cap, 0u);
-    mask_ = cap - 1;
-  }
-  // Position in `firstRows` of the first row whose key equals keys[row]; if
-  // there is none, appends `row` to firstRows and returns kNone.
-  uint32_t findOrAdd(std::vector<Hash> const& keys, size_t row, std::vector<size_t>& firstRows) {
-    Hash const& k = keys[row];
-    for (size_t s = keyBits(k) & mask_;; s = (s + 1) & mask_) {
-      if (slot_[s] == 0) {
-        slot_[s] = (uint32_t)firstRows.size() + 1;
-        firstRows.push_back(row);
-        return kNone;
-      }
-      if (keys[firstRows[slot_[s] - 1]] == k) return slot_[s] - 1;
-    }
-  }
-
- private:
-  size_t mask_;
-  std::vector<uint32_t> slot_;  // position in firstRows + 1; 0 = empty
-};
-
 std::mutex gVerifySigCacheMutex;
 RandomEvictionCache gVerifySigCache(0xffff);
 uint64_t gVerifyCacheHit = 0;
 uint64_t gVerifyCacheMiss = 0;
-uint64_t gEngineSigs = 0;
-uint64_t gEngineBatches = 0;
+uint64_t gBatchId = 0;  // owner ids of pending entries (under the mutex)
+std::atomic<uint64_t> gGpuSigs{0}, gGpuBatches{0}, gCpuSigs{0}, gFallbacks{0};
 std::atomic<PubKeyUtils::BatchVerifyFn> gTestVerifier{nullptr};
 std::atomic<PubKeyUtils::KeyedBatchVerifyFn> gTestKeyedVerifier{nullptr};
-std::atomic<size_t> gKeyedThreshold{4096};
+std::atomic<size_t> gKeyedThreshold{256};
+std::atomic<size_t> gCpuThreshold{1};
+
+using Item = PubKeyUtils::VerifyItem;
+
+// SoA copy of items[rows] for the test hooks (the engine itself gathers).
+struct Packed {
+  std::vector<uint8_t> pk, sig, msg;
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> len;
+  Packed(std::vector<Item> const& items, std::vector<size_t> const& rows) {
+    const size_t n = rows.size();
+    pk.resize(32 * n);
+    sig.resize(64 * n);
+    off.resize(n);
+    len.resize(n);
+    size_t total = 0;
+    for (size_t r : rows) total += items[r].msg.size();
+    msg.resize(std::max<size_t>(1, total));
+    size_t pos = 0;
+    for (size_t i = 0; i < n; ++i) {
+      Item const& it = items[rows[i]];
+      std::memcpy(&pk[32 * i], it.key->ed25519().data(), 32);
+      std::memcpy(&sig[64 * i], it.signature->data(), 64);
+      off[i] = pos;
+      len[i] = (uint32_t)it.msg.size();
+      if (len[i]) std::memcpy(&msg[pos], it.msg.data(), len[i]);
+      pos += len[i];
+    }
+  }
+};
+
+// CPU path over items[rows] (the engine's own algorithm, host build).
+void cpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, uint8_t* verdict) {
+  parallelFor(rows.size(), 4, [&](size_t i) {
+    Item const& it = items[rows[i]];
+    verdict[i] = sv_ed25519_verify_cpu(it.key->ed25519().data(), it.signature->data(), it.msg.data(),
+                                       it.msg.size()) == 1
+                     ? 1
+                     : 0;
+  });
+  gCpuSigs += rows.size();
+}
+
+void hostKeys(std::vector<Item> const& items, std::vector<size_t> const& rows, Hash* keys) {
+  parallelFor(rows.size(), 256, [&](size_t i) {
+    Item const& it = items[rows[i]];
+    keys[i] = PubKeyUtils::verifySigCacheKey(*it.key, *it.signature, it.msg);
+  });
+}
+
+// GPU engine over items[rows] (gather: the engine packs straight from the
+// items); keys != nullptr also returns the cache keys.  Returns the engine's
+// status; the caller falls back to the CPU path on any error.
+int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, uint8_t* verdict, Hash* keys) {
+  const size_t n = rows.size();
+  static_assert(sizeof(Hash) == 32, "Hash must be 32 contiguous bytes");
+  uint8_t* kb = reinterpret_cast<uint8_t*>(keys);
+  if (keys) {
+    if (PubKeyUtils::KeyedBatchVerifyFn tk = gTestKeyedVerifier.load()) {
+      Packed p(items, rows);
+      return tk(p.pk.data(), p.sig.data(), p.msg.data(), p.off.data(), p.len.data(), n, verdict, kb);
+    }
+  } else if (PubKeyUtils::BatchVerifyFn tv = gTestVerifier.load()) {
+    Packed p(items, rows);
+    return tv(p.pk.data(), p.sig.data(), p.msg.data(), p.off.data(), p.len.data(), n, verdict);
+  }
+  std::vector<const uint8_t*> pk(n), sig(n), msg(n);
+  std::vector<uint32_t> len(n);
+  for (size_t i = 0; i < n; ++i) {
+    Item const& it = items[rows[i]];
+    pk[i] = it.key->ed25519().data();
+    sig[i] = it.signature->data();
+    msg[i] = it.msg.data();
+    len[i] = (uint32_t)it.msg.size();
+  }
+  return sv_ed25519_verify_batch_gather(pk.data(), sig.data(), msg.data(), len.data(), n, verdict, kb, nullptr);
+}
+
+}  // namespace
+
+namespace PubKeyUtils {
 
 Hash verifySigCacheKey(PublicKey const& key, Signature const& signature, ByteSlice const& bin) {
   hostcrypto::Blake2b256 h;
@@ -187,168 +352,133 @@ Hash verifySigCacheKey(PublicKey const& key, Signature const& signature, ByteSli
   return h.finish();
 }
 
-// Per-thread staging for engine calls: reused across calls so a large batch
-// does not pay fresh page faults for ~200 B/signature of packing buffers.
-struct Staging {
-  std::vector<uint8_t> pk, sig, msg;
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> len;
-};
-Staging& staging() {
-  static thread_local Staging st;
-  return st;
-}
-
-// Sends `items` to the engine (GPU) in one batch.  With `keys` non-null the
-// engine also returns each item's BLAKE2b cache key (keyed pass, f4), written
-// to keys[0..n) (Hash is 32 contiguous bytes).
-void dispatch(std::vector<PubKeyUtils::VerifyItem const*> const& items, std::vector<uint8_t>& verdict,
-              Hash* keys = nullptr) {
-  const size_t n = items.size();
-  verdict.assign(n, 0);
-  if (n == 0) return;
-  Staging& st = staging();
-  st.pk.resize(32 * n);
-  st.sig.resize(64 * n);
-  st.off.resize(n);
-  st.len.resize(n);
-  size_t total = 0;
-  bool all32 = true;
-  for (size_t i = 0; i < n; ++i) {
-    total += items[i]->msg.size();
-    all32 = all32 && items[i]->msg.size() == 32;
-  }
-  st.msg.resize(total ? total : 1);
-  size_t pos = 0;
-  for (size_t i = 0; i < n; ++i) {
-    std::memcpy(&st.pk[32 * i], items[i]->key->ed25519().data(), 32);
-    std::memcpy(&st.sig[64 * i], items[i]->signature->data(), 64);
-    st.off[i] = pos;
-    st.len[i] = (uint32_t)items[i]->msg.size();
-    if (st.len[i]) std::memcpy(&st.msg[pos], items[i]->msg.data(), st.len[i]);
-    pos += st.len[i];
-  }
-  int rc;
-  bool testing = false;
-  static_assert(sizeof(Hash) == 32, "Hash must be 32 contiguous bytes");
-  if (keys) {
-    uint8_t* kb = reinterpret_cast<uint8_t*>(keys);
-    PubKeyUtils::KeyedBatchVerifyFn tk = gTestKeyedVerifier.load();
-    testing = tk != nullptr;
-    rc = tk ? tk(st.pk.data(), st.sig.data(), st.msg.data(), st.off.data(), st.len.data(), n, verdict.data(), kb)
-            : sv_ed25519_verify_batch_keyed(st.pk.data(), st.sig.data(), st.msg.data(), st.off.data(),
-                                            st.len.data(), n, verdict.data(), kb, nullptr);
-  } else {
-    PubKeyUtils::BatchVerifyFn tv = gTestVerifier.load();
-    testing = tv != nullptr;
-    if (tv) {
-      rc = tv(st.pk.data(), st.sig.data(), st.msg.data(), st.off.data(), st.len.data(), n, verdict.data());
-    } else if (all32) {
-      rc = sv_ed25519_verify_batch_fixed(st.pk.data(), st.sig.data(), st.msg.data(), 32, n, verdict.data(),
-                                         nullptr);
-    } else {
-      rc = sv_ed25519_verify_batch(st.pk.data(), st.sig.data(), st.msg.data(), st.off.data(), st.len.data(), n,
-                                   verdict.data(), nullptr);
-    }
-  }
-  if (rc != SV_OK) {
-    throw VerifyEngineError(std::string("ed25519 batch verification failed (") + std::to_string(rc) +
-                            "): " + (testing ? "test verifier" : sv_last_error_string()));
-  }
-}
-
-}  // namespace
-
-namespace PubKeyUtils {
-
-std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items) {
+std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vector<Hash>* keysOut) {
   const size_t n = items.size();
   std::vector<bool> out(n, false);
-  std::vector<Hash> keys(n);
-  std::vector<VerifyItem const*> eligible;
-  std::vector<size_t> eligibleRow;
+  std::vector<size_t> rows;  // eligible items
+  rows.reserve(n);
   for (size_t i = 0; i < n; ++i) {
     if (items[i].key->type() != PUBLIC_KEY_TYPE_ED25519)
       throw std::invalid_argument("verifySigBatch: non-ed25519 key");  // releaseAssert, SecretKey.cpp:440
     if (items[i].signature->size() != 64) continue;                   // SecretKey.cpp:441-444
-    eligible.push_back(&items[i]);
-    eligibleRow.push_back(i);
+    rows.push_back(i);
   }
+  if (keysOut) keysOut->assign(n, Hash{});
+  const size_t E = rows.size();
+  if (E == 0) return out;
+  std::vector<Hash> keys(E);
+  std::vector<uint8_t> verdict(E, 0);
+
   const size_t thr = gKeyedThreshold.load();
-  const bool keyed = thr != 0 && eligible.size() >= thr && gTestVerifier.load() == nullptr;
-  std::vector<uint8_t> keyedVerdict;
-  if (keyed) {
-    // one engine pass over every eligible row: verdicts + cache keys (f4)
-    if (eligible.size() == n) {
-      dispatch(eligible, keyedVerdict, keys.data());
+  if (thr != 0 && E >= thr && gTestVerifier.load() == nullptr) {
+    // keyed: every eligible item verified and hashed in one engine pass
+    if (gpuVerify(items, rows, verdict.data(), keys.data()) == SV_OK) {
+      gGpuSigs += E;
+      gGpuBatches += 1;
     } else {
-      std::vector<Hash> ek(eligible.size());
-      dispatch(eligible, keyedVerdict, ek.data());
-      for (size_t e = 0; e < eligible.size(); ++e) keys[eligibleRow[e]] = ek[e];
+      ++gFallbacks;
+      hostKeys(items, rows, keys.data());
+      cpuVerify(items, rows, verdict.data());
+    }
+    std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
+    for (size_t e = 0; e < E; ++e) {
+      if (e + 8 < E) gVerifySigCache.prefetch(keys[e + 8]);
+      const uint32_t id = gVerifySigCache.find(keys[e]);
+      if (id != RandomEvictionCache::kNone && gVerifySigCache.at(id).owner == 0) {
+        ++gVerifyCacheHit;
+        out[rows[e]] = gVerifySigCache.touch(id).value;
+      } else {
+        ++gVerifyCacheMiss;
+        gVerifySigCache.put(keys[e], verdict[e] != 0);
+        out[rows[e]] = verdict[e] != 0;
+      }
     }
   } else {
-    // hashed outside the cache lock
-    for (size_t r : eligibleRow) keys[r] = verifySigCacheKey(*items[r].key, *items[r].signature, items[r].msg);
-  }
-  std::vector<int64_t> missSlot(n, -1);  // index into `misses` for rows resolved by the engine
-  std::vector<size_t> misses;            // row of each distinct miss
-  {
-    BatchFirstIndex batchFirst(eligibleRow.size());  // duplicates inside this batch
-    std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
-    for (size_t e = 0; e < eligibleRow.size(); ++e) {
-      const size_t i = eligibleRow[e];
-      if (e + 8 < eligibleRow.size()) gVerifySigCache.prefetch(keys[eligibleRow[e + 8]]);
-      if (gVerifySigCache.exists(keys[i])) {
-        ++gVerifyCacheHit;
-        out[i] = gVerifySigCache.get(keys[i]);
-        continue;
-      }
-      const uint32_t first = batchFirst.findOrAdd(keys, i, misses);
-      if (first != BatchFirstIndex::kNone) {
-        // a sequential caller would hit the entry its first occurrence stored
-        ++gVerifyCacheHit;
-        missSlot[i] = (int64_t)first;
-        continue;
-      }
-      missSlot[i] = (int64_t)(misses.size() - 1);
-    }
-    if (keyed) {
-      // verdicts are already here: finish under the same lock
-      std::vector<uint8_t> rowVerdict(n, 0);
-      for (size_t e = 0; e < eligible.size(); ++e) rowVerdict[eligibleRow[e]] = keyedVerdict[e];
-      gEngineSigs += eligible.size();
-      gEngineBatches += 1;
-      for (size_t m : misses) {
+    hostKeys(items, rows, keys.data());
+    // phase 1: walk the cache in item order; misses are inserted pending
+    std::vector<size_t> missRows;  // item of each distinct miss
+    std::vector<uint32_t> ref(E, RandomEvictionCache::kNone);
+    uint64_t owner;
+    {
+      std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
+      owner = ++gBatchId;
+      for (size_t e = 0; e < E; ++e) {
+        if (e + 8 < E) gVerifySigCache.prefetch(keys[e + 8]);
+        const uint32_t id = gVerifySigCache.find(keys[e]);
+        if (id != RandomEvictionCache::kNone) {
+          auto const& ent = gVerifySigCache.at(id);
+          if (ent.owner == 0) {
+            ++gVerifyCacheHit;
+            out[rows[e]] = gVerifySigCache.touch(id).value;
+            continue;
+          }
+          if (ent.owner == owner) {  // an earlier item of this batch
+            ++gVerifyCacheHit;
+            ref[e] = gVerifySigCache.touch(id).pendIdx;
+            continue;
+          }
+        }
         ++gVerifyCacheMiss;
-        gVerifySigCache.put(keys[m], rowVerdict[m] != 0);
+        ref[e] = (uint32_t)missRows.size();
+        gVerifySigCache.put(keys[e], false, owner, ref[e]);
+        missRows.push_back(e);
       }
-      for (size_t i = 0; i < n; ++i)
-        if (missSlot[i] >= 0) out[i] = rowVerdict[misses[(size_t)missSlot[i]]] != 0;
-      return out;
     }
+    // phase 2: verify the misses (outside the lock: the engine call is long)
+    const size_t M = missRows.size();
+    std::vector<size_t> missItems(M);
+    for (size_t m = 0; m < M; ++m) missItems[m] = rows[missRows[m]];
+    std::vector<uint8_t> mv(M, 0);
+    if (M > 0) {
+      if (M <= gCpuThreshold.load() && gTestVerifier.load() == nullptr) {
+        cpuVerify(items, missItems, mv.data());
+      } else if (gpuVerify(items, missItems, mv.data(), nullptr) == SV_OK) {
+        gGpuSigs += M;
+        gGpuBatches += 1;
+      } else {
+        ++gFallbacks;
+        cpuVerify(items, missItems, mv.data());
+      }
+    }
+    // phase 3: fill in the pending values
+    {
+      std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
+      for (size_t m = 0; m < M; ++m) gVerifySigCache.resolve(keys[missRows[m]], owner, (uint32_t)m, mv[m] != 0);
+    }
+    for (size_t e = 0; e < E; ++e)
+      if (ref[e] != RandomEvictionCache::kNone) out[rows[e]] = mv[ref[e]] != 0;
   }
-  std::vector<VerifyItem const*> missItems;
-  missItems.reserve(misses.size());
-  for (size_t m : misses) missItems.push_back(&items[m]);
-  std::vector<uint8_t> verdict;
-  dispatch(missItems, verdict);  // outside the lock: the engine call is long
-  std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
-  if (!misses.empty()) {
-    gEngineSigs += misses.size();
-    gEngineBatches += 1;
-  }
-  for (size_t m = 0; m < misses.size(); ++m) {
-    ++gVerifyCacheMiss;
-    gVerifySigCache.put(keys[misses[m]], verdict[m] != 0);
-  }
-  for (size_t i = 0; i < n; ++i)
-    if (missSlot[i] >= 0) out[i] = verdict[(size_t)missSlot[i]] != 0;
+  if (keysOut)
+    for (size_t e = 0; e < E; ++e) (*keysOut)[rows[e]] = keys[e];
   return out;
+}
+
+std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items) { return verifySigBatch(items, nullptr); }
+
+void verifyBatchUncached(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                         const uint32_t* len, size_t n, uint8_t* verdict) {
+  if (n == 0) return;
+  BatchVerifyFn tv = gTestVerifier.load();
+  if (!tv && n <= gCpuThreshold.load()) {
+    sv_ed25519_verify_batch_cpu(pk, sig, msg, off, len, n, verdict, 0);
+    gCpuSigs += n;
+    return;
+  }
+  const int rc = tv ? tv(pk, sig, msg, off, len, n, verdict)
+                    : sv_ed25519_verify_batch(pk, sig, msg, off, len, n, verdict, nullptr);
+  if (rc == SV_OK) {
+    gGpuSigs += n;
+    gGpuBatches += 1;
+    return;
+  }
+  ++gFallbacks;
+  sv_ed25519_verify_batch_cpu(pk, sig, msg, off, len, n, verdict, 0);
+  gCpuSigs += n;
 }
 
 bool verifySig(PublicKey const& key, Signature const& signature, ByteSlice const& bin) {
   std::vector<VerifyItem> one{VerifyItem{&key, &signature, bin}};
-  return verifySigBatch(one)[0];
+  return verifySigBatch(one, nullptr)[0];
 }
 
 void clearVerifySigCache() {
@@ -372,13 +502,25 @@ void flushVerifySigCacheCounts(uint64_t& hits, uint64_t& misses) {
 void setBatchVerifierForTesting(BatchVerifyFn fn) { gTestVerifier.store(fn); }
 void setKeyedBatchVerifierForTesting(KeyedBatchVerifyFn fn) { gTestKeyedVerifier.store(fn); }
 void setKeyedBatchThreshold(size_t minItems) { gKeyedThreshold.store(minItems); }
+void setCpuBatchThreshold(size_t maxMisses) { gCpuThreshold.store(maxMisses); }
+
+EngineCounts flushEngineCounts() {
+  EngineCounts c;
+  c.gpuSignatures = gGpuSigs.exchange(0);
+  c.gpuBatches = gGpuBatches.exchange(0);
+  c.cpuSignatures = gCpuSigs.exchange(0);
+  c.fallbacks = gFallbacks.exchange(0);
+  return c;
+}
 
 void flushEngineCounts(uint64_t& signatures, uint64_t& batches) {
+  signatures = gGpuSigs.exchange(0);
+  batches = gGpuBatches.exchange(0);
+}
+
+std::vector<Hash> cacheKeysForTesting() {
   std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
-  signatures = gEngineSigs;
-  batches = gEngineBatches;
-  gEngineSigs = 0;
-  gEngineBatches = 0;
+  return gVerifySigCache.keysInOrder();
 }
 
 }  // namespace PubKeyUtils

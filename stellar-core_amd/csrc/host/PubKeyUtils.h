@@ -12,10 +12,21 @@
 //
 // Semantics kept from SecretKey.cpp:435-468: a signature whose size != 64 is
 // rejected before any cache interaction; the cache key is BLAKE2b-256(pk ||
-// sig || msg); the process-global 0xffff-entry random-eviction cache is
-// consulted before dispatch; BOTH verdicts are stored; hit/miss counters.
-// Difference: misses go to the GPU engine in one batch, and a device error is
-// thrown as VerifyEngineError (never turned into a reject).
+// sig || msg); the process-global 0xffff-entry random-eviction cache
+// (RandomEvictionCache.h, two draws of the libc++ uniform_int_distribution
+// stellar-core pins in lib/util/stdrandom.h) is consulted before dispatch and
+// BOTH verdicts are stored; hit/miss counters.  verifySigBatch(items) leaves
+// the cache, its counters and the verdicts exactly as the same items passed
+// one by one to verifySig would (tests/test_host_mirror.py replays it against
+// a sequential restatement of the reference cache).
+//
+// Like the reference, nothing here throws on a verification problem:
+// misses go to the GPU engine in one batch; a single miss (or any batch of at
+// most cpuBatchThreshold misses) runs on the engine's CPU path
+// (sv_ed25519_verify_batch_cpu: the same algorithm compiled for the host,
+// cheaper than a GPU round trip); if the GPU engine returns an error the batch
+// is re-run on the CPU path -- an engine error is never a reject and never an
+// exception.  engineFallbacks counts those re-runs.
 #pragma once
 
 #include <array>
@@ -58,11 +69,6 @@ struct ByteSlice {
   const uint8_t* end() const { return p + n; }
 };
 
-class VerifyEngineError : public std::runtime_error {
- public:
-  explicit VerifyEngineError(std::string const& m) : std::runtime_error(m) {}
-};
-
 namespace PubKeyUtils {
 
 struct VerifyItem {
@@ -73,32 +79,60 @@ struct VerifyItem {
 
 bool verifySig(PublicKey const& key, Signature const& signature, ByteSlice const& bin);
 std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items);
+// Same, also returning every item's verify-cache key (keysOut[i]; items whose
+// signature size != 64 get an all-zero key) -- for callers that index their
+// own side tables by it without hashing again.
+std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vector<Hash>* keysOut);
+
+// Engine-only batch over contiguous SoA buffers (message i = msg[off[i] ..
+// off[i] + len[i])), no cache interaction: the GPU engine (or the test
+// verifier), the CPU path for at most cpuBatchThreshold items or on an engine
+// error.  Callers that keep their own verdict tables (SignatureBatchPrefetch,
+// catchup replay) use this.
+void verifyBatchUncached(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                         const uint32_t* len, size_t n, uint8_t* verdict);
 
 void clearVerifySigCache();
 void maybeSeedVerifySigCache(unsigned int seed);
 void flushVerifySigCacheCounts(uint64_t& hits, uint64_t& misses);
 
+// BLAKE2b-256(pk || sig || msg), SecretKey.cpp:50-61
+Hash verifySigCacheKey(PublicKey const& key, Signature const& signature, ByteSlice const& bin);
+
 // Engine override for tests (cf. the reference's BUILD_TESTS hooks such as
-// AlwaysValidSignatureChecker, SignatureChecker.h:41-63): when set, cache
-// misses are sent to `fn` instead of the GPU.  Pass nullptr to restore.
+// AlwaysValidSignatureChecker, SignatureChecker.h:41-63): when set, GPU-bound
+// misses are sent to `fn` instead of the GPU.  A non-zero return is treated
+// like an engine error (CPU fallback).  Pass nullptr to restore.
 using BatchVerifyFn = int (*)(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
                               const uint32_t* len, size_t n, uint8_t* verdict);
 void setBatchVerifierForTesting(BatchVerifyFn fn);
 
 // Keyed batches: a verifySigBatch call with at least
 // `minItems` eligible signatures sends ALL of them to the engine in one pass
-// that returns verdicts AND the BLAKE2b cache keys (sv_ed25519_verify_batch_keyed),
-// so the host never hashes; cache bookkeeping (hits, in-batch duplicates,
-// misses, insertions, counters) is then identical to the hashed path.
-// 0 disables.  Default 4096.
+// that returns verdicts AND the BLAKE2b cache keys (sv_ed25519_verify_batch_gather
+// with keys), so the host never hashes; the cache is then walked once in item
+// order, exactly as sequential verifySig calls would.  0 disables.  Default 256.
 void setKeyedBatchThreshold(size_t minItems);
 using KeyedBatchVerifyFn = int (*)(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
                                    const uint32_t* len, size_t n, uint8_t* verdict, uint8_t* keys);
 void setKeyedBatchVerifierForTesting(KeyedBatchVerifyFn fn);
 
-// Number of signatures sent to the engine and number of engine calls
-// (batches) since the last flush -- observability for batch sizes.
+// Batches with at most this many cache misses run on the CPU path instead of
+// the GPU (default 1: a single verifySig never pays a GPU round trip).
+void setCpuBatchThreshold(size_t maxMisses);
+
+// Observability: signatures sent to the GPU engine, engine calls (batches),
+// signatures verified on the CPU path, and engine errors that were re-run on
+// the CPU path, since the last flush.
+struct EngineCounts {
+  uint64_t gpuSignatures = 0, gpuBatches = 0, cpuSignatures = 0, fallbacks = 0;
+};
+EngineCounts flushEngineCounts();
 void flushEngineCounts(uint64_t& signatures, uint64_t& batches);
+
+// Test hook: cache keys currently held, in the cache's insertion-order vector
+// (the reference's mValuePtrs), for replay tests of the eviction policy.
+std::vector<Hash> cacheKeysForTesting();
 
 }  // namespace PubKeyUtils
 }  // namespace stellar

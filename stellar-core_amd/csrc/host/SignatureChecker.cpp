@@ -5,7 +5,6 @@
 
 #include <cstring>
 #include <functional>
-#include <string>
 
 #include "hashes.h"
 
@@ -37,24 +36,57 @@ SignatureHint getSignedPayloadHint(SignerKey const& s) {
   return h;
 }
 
+// SignatureUtils.cpp:38-46
+bool verify(DecoratedSignature const& sig, SignerKey const& signerKey, Hash const& hash) {
+  if (!doesHintMatch(ByteSlice(signerKey.key.data(), 32), sig.hint)) return false;
+  PublicKey pk;
+  pk.ed25519() = signerKey.key;
+  return PubKeyUtils::verifySig(pk, sig.signature, ByteSlice(hash.data(), hash.size()));
+}
+
+// SignatureUtils.cpp:86-93
+bool verifyHashX(DecoratedSignature const& sig, SignerKey const& signerKey) {
+  if (!doesHintMatch(ByteSlice(signerKey.key.data(), 32), sig.hint)) return false;
+  auto h = hostcrypto::sha256(sig.signature.data(), sig.signature.size());
+  return std::memcmp(h.data(), signerKey.key.data(), 32) == 0;
+}
+
+// SignatureUtils.cpp:48-61
+bool verifyEd25519SignedPayload(DecoratedSignature const& sig, SignerKey const& signer) {
+  SignatureHint h = getSignedPayloadHint(signer);
+  if (!doesHintMatch(ByteSlice(h.data(), 4), sig.hint)) return false;
+  PublicKey pk;
+  pk.ed25519() = signer.key;
+  return PubKeyUtils::verifySig(pk, sig.signature, ByteSlice(signer.payload.data(), signer.payload.size()));
+}
+
 }  // namespace SignatureUtils
 
 namespace {
-
-std::string cacheKeyString(uint256 const& pk, Signature const& sig, ByteSlice const& msg) {
-  hostcrypto::Blake2b256 h;
-  h.add(pk.data(), 32);
-  h.add(sig.data(), sig.size());
-  h.add(msg.data(), msg.size());
-  auto d = h.finish();
-  return std::string(reinterpret_cast<const char*>(d.data()), d.size());
-}
-
 uint32_t clampWeight(uint32_t protocol, uint32_t w) { return (protocol >= 10 && w > 255) ? 255 : w; }
-
 }  // namespace
 
 // ---------------------------------------------------------------- prefetch
+uint64_t SignatureBatchPrefetch::hashOf(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, size_t len) {
+  // signatures and keys are uniformly distributed bytes: a few words of each
+  // (plus the message's) make a good table hash; lookups compare all bytes
+  uint64_t a, b, c = 0;
+  std::memcpy(&a, sig, 8);
+  std::memcpy(&b, pk + 24, 8);
+  if (len >= 8) std::memcpy(&c, msg + len - 8, 8);
+  else if (len) std::memcpy(&c, msg, len);
+  uint64_t h = a ^ (b * 0x9e3779b97f4a7c15ull) ^ ((c + len) * 0xc2b2ae3d27d4eb4full);
+  return h ^ (h >> 29);
+}
+
+void SignatureBatchPrefetch::push(uint256 const& pk, Signature const& sig, const uint8_t* msg, size_t msgLen) {
+  pk_.insert(pk_.end(), pk.begin(), pk.end());
+  sig_.insert(sig_.end(), sig.begin(), sig.end());
+  off_.push_back(msg_.size());
+  len_.push_back((uint32_t)msgLen);
+  msg_.insert(msg_.end(), msg, msg + msgLen);
+}
+
 void SignatureBatchPrefetch::add(Hash const& contentsHash, std::vector<DecoratedSignature> const& signatures,
                                  std::vector<Signer> const& signers) {
   for (auto const& sig : signatures) {
@@ -62,40 +94,62 @@ void SignatureBatchPrefetch::add(Hash const& contentsHash, std::vector<Decorated
     for (auto const& s : signers) {
       if (s.key.type == SIGNER_KEY_TYPE_ED25519) {
         if (!SignatureUtils::doesHintMatch(ByteSlice(s.key.key.data(), 32), sig.hint)) continue;
-        Pending p;
-        p.pk.ed25519() = s.key.key;
-        p.sig = sig.signature;
-        p.msg.assign(contentsHash.begin(), contentsHash.end());
-        items_.push_back(std::move(p));
+        push(s.key.key, sig.signature, contentsHash.data(), 32);
       } else if (s.key.type == SIGNER_KEY_TYPE_ED25519_SIGNED_PAYLOAD) {
         SignatureHint h = SignatureUtils::getSignedPayloadHint(s.key);
         if (!SignatureUtils::doesHintMatch(ByteSlice(h.data(), 4), sig.hint)) continue;
-        Pending p;
-        p.pk.ed25519() = s.key.key;
-        p.sig = sig.signature;
-        p.msg = s.key.payload;
-        items_.push_back(std::move(p));
+        push(s.key.key, sig.signature, s.key.payload.data(), s.key.payload.size());
       }
     }
   }
 }
 
-void SignatureBatchPrefetch::run() {
-  std::vector<PubKeyUtils::VerifyItem> items;
-  items.reserve(items_.size());
-  for (auto const& p : items_) items.push_back(PubKeyUtils::VerifyItem{&p.pk, &p.sig, ByteSlice(p.msg)});
-  std::vector<bool> v = PubKeyUtils::verifySigBatch(items);
-  verdicts_.reserve(items_.size());
-  for (size_t i = 0; i < items_.size(); ++i)
-    verdicts_[cacheKeyString(items_[i].pk.ed25519(), items_[i].sig, ByteSlice(items_[i].msg))] = v[i];
+void SignatureBatchPrefetch::run(bool seedCache) {
+  const size_t n = len_.size();
+  verdict_.assign(n, 0);
+  if (n == 0) return;
+  const uint8_t* msg = msg_.empty() ? nullptr : msg_.data();
+  if (seedCache) {
+    std::vector<PublicKey> keys(n);
+    std::vector<Signature> sigs(n);
+    std::vector<PubKeyUtils::VerifyItem> items(n);
+    for (size_t i = 0; i < n; ++i) {
+      std::memcpy(keys[i].ed25519().data(), &pk_[32 * i], 32);
+      sigs[i].assign(&sig_[64 * i], &sig_[64 * i] + 64);
+      items[i] = PubKeyUtils::VerifyItem{&keys[i], &sigs[i], ByteSlice(msg ? msg + off_[i] : nullptr, len_[i])};
+    }
+    std::vector<bool> v = PubKeyUtils::verifySigBatch(items);
+    for (size_t i = 0; i < n; ++i) verdict_[i] = v[i] ? 1 : 0;
+  } else {
+    static const uint8_t dummy = 0;
+    PubKeyUtils::verifyBatchUncached(pk_.data(), sig_.data(), msg ? msg : &dummy, off_.data(), len_.data(), n,
+                                     verdict_.data());
+  }
+  size_t cap = 16;
+  while (cap < 2 * n) cap <<= 1;
+  mask_ = cap - 1;
+  table_.assign(cap, 0u);
+  for (size_t i = 0; i < n; ++i) {
+    size_t s = hashOf(&pk_[32 * i], &sig_[64 * i], msg ? msg + off_[i] : nullptr, len_[i]) & mask_;
+    while (table_[s] != 0) s = (s + 1) & mask_;
+    table_[s] = (uint32_t)(i + 1);
+  }
 }
 
 bool SignatureBatchPrefetch::lookup(uint256 const& pk, Signature const& sig, ByteSlice const& msg,
                                     bool& verdict) const {
-  auto it = verdicts_.find(cacheKeyString(pk, sig, msg));
-  if (it == verdicts_.end()) return false;
-  verdict = it->second;
-  return true;
+  if (table_.empty() || sig.size() != 64) return false;
+  for (size_t s = hashOf(pk.data(), sig.data(), msg.data(), msg.size()) & mask_;; s = (s + 1) & mask_) {
+    const uint32_t t = table_[s];
+    if (t == 0) return false;
+    const size_t i = t - 1;
+    if (len_[i] == msg.size() && std::memcmp(&sig_[64 * i], sig.data(), 64) == 0 &&
+        std::memcmp(&pk_[32 * i], pk.data(), 32) == 0 &&
+        (msg.size() == 0 || std::memcmp(&msg_[off_[i]], msg.data(), msg.size()) == 0)) {
+      verdict = verdict_[i] != 0;
+      return true;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- checker
@@ -150,10 +204,7 @@ bool SignatureChecker::checkSignature(std::vector<Signer> const& signersV, int32
   };
 
   if (verifyAll(byType[SIGNER_KEY_TYPE_HASH_X], [&](DecoratedSignature const& sig, Signer const& s) {
-        // SignatureUtils::verifyHashX, SignatureUtils.cpp:86-93
-        if (!SignatureUtils::doesHintMatch(ByteSlice(s.key.key.data(), 32), sig.hint)) return false;
-        auto h = hostcrypto::sha256(sig.signature.data(), sig.signature.size());
-        return std::memcmp(h.data(), s.key.key.data(), 32) == 0;
+        return SignatureUtils::verifyHashX(sig, s.key);
       }))
     return true;
 

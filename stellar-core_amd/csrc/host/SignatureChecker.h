@@ -17,12 +17,13 @@
 // 1582-1648), verifies them in one GPU batch, and hands the verdicts to the
 // checkers as a side table -- so the per-tx checkers never wait on the GPU
 // one signature at a time, and the 0xffff-entry global cache cannot evict a
-// verdict before it is used.
+// verdict before it is used.  The side table is keyed by the (pk, sig, msg)
+// bytes themselves (a cheap hash of them, full compare on lookup), not by the
+// BLAKE2b cache key, so a checker's lookup costs no hashing.
 #pragma once
 
 #include <array>
 #include <cstdint>
-#include <unordered_map>
 #include <vector>
 
 #include "PubKeyUtils.h"
@@ -58,30 +59,37 @@ namespace SignatureUtils {
 SignatureHint getHint(ByteSlice const& bs);
 bool doesHintMatch(ByteSlice const& bs, SignatureHint const& hint);
 SignatureHint getSignedPayloadHint(SignerKey const& signedPayloadSigner);
+// SignatureUtils::verify / verifyHashX / verifyEd25519SignedPayload
+bool verify(DecoratedSignature const& sig, SignerKey const& signerKey, Hash const& hash);
+bool verifyHashX(DecoratedSignature const& sig, SignerKey const& signerKey);
+bool verifyEd25519SignedPayload(DecoratedSignature const& sig, SignerKey const& signer);
 }  // namespace SignatureUtils
 
-// Verdicts computed ahead of the checkers, keyed by the verify-cache key
-// BLAKE2b-256(pk || sig || msg).
+// Verdicts computed ahead of the checkers.
 class SignatureBatchPrefetch {
  public:
   // Enumerate the hint-matching ed25519 / signed-payload pairs of one tx.
   void add(Hash const& contentsHash, std::vector<DecoratedSignature> const& signatures,
            std::vector<Signer> const& signers);
-  // One GPU batch over everything added (through PubKeyUtils::verifySigBatch,
-  // so the global cache is filled too).
-  void run();
+  // One engine batch over everything added.  seedCache = false: the verdicts
+  // go to the side table only (the engine is called directly, no cache
+  // interaction); true: through PubKeyUtils::verifySigBatch, which also fills
+  // the global verify cache (a later verifySig then hits).  An engine error
+  // re-runs the batch on the CPU path.
+  void run(bool seedCache = false);
   // verdict for (pk, sig, msg) if prefetched
   bool lookup(uint256 const& pk, Signature const& sig, ByteSlice const& msg, bool& verdict) const;
-  size_t pairs() const { return items_.size(); }
+  size_t pairs() const { return len_.size(); }
 
  private:
-  struct Pending {
-    PublicKey pk;
-    Signature sig;
-    std::vector<uint8_t> msg;
-  };
-  std::vector<Pending> items_;
-  std::unordered_map<std::string, bool> verdicts_;
+  void push(uint256 const& pk, Signature const& sig, const uint8_t* msg, size_t msgLen);
+  static uint64_t hashOf(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, size_t len);
+  std::vector<uint8_t> pk_, sig_, msg_;
+  std::vector<uint64_t> off_;
+  std::vector<uint32_t> len_;
+  std::vector<uint8_t> verdict_;
+  std::vector<uint32_t> table_;  // open addressing: pair index + 1, 0 = empty
+  size_t mask_ = 0;
 };
 
 class SignatureChecker {

@@ -4,16 +4,18 @@
 // SCP_MESSAGE signature one by one and discards the result only to warm the
 // global verify cache (/root/reference/src/overlay/Peer.cpp:963-970); the main
 // thread's HerderImpl::verifyEnvelope (src/herder/HerderImpl.cpp:2414-2432)
-// then hits the cache.  Here producers enqueue (pk, sig, msg) and get a
-// future; a worker thread flushes the queue as ONE PubKeyUtils::verifySigBatch
-// call (which also fills the cache) when it holds maxBatch items or when the
-// oldest item has waited maxDelay -- whichever comes first.  With workers > 1
-// several batches are in flight at once: one worker's host work (cache keys,
-// cache lookups, packing, promise fulfilment) overlaps another's engine call.
-// The engine and the verify cache are thread-safe, so verdicts do not depend
-// on the worker count.  Default 2: with one worker a flood of 1k-item batches
-// queued up behind the host work (p50 submit->verdict 229 ms at 0.31M/s); two
-// measured 2.1 ms at 0.68M/s (tools/bench_configs.py configmb).
+// then hits the cache.  Here producers enqueue (pk, sig, msg) -- post() when
+// the result is only meant to warm the cache, exactly like the reference's
+// pre-verify, or submit() for a future carrying the verdict -- and a worker
+// thread flushes the queue as ONE PubKeyUtils::verifySigBatch call (which also
+// fills the cache) when it holds maxBatch items or when the oldest has waited
+// maxDelay, whichever comes first.  With workers > 1 several batches are in
+// flight at once: one worker's host work (cache walk, promise fulfilment)
+// overlaps another's engine call.  The engine and the verify cache are
+// thread-safe, so verdicts do not depend on the worker count.
+//
+// Engine errors never reach producers: verifySigBatch re-runs a failed batch
+// on the CPU path (PubKeyUtils.h).
 #pragma once
 
 #include <chrono>
@@ -21,6 +23,7 @@
 #include <cstdint>
 #include <deque>
 #include <future>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -31,13 +34,20 @@ namespace stellar {
 
 class VerifyMicroBatcher {
  public:
-  VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay, unsigned workers = 2);
+  // recordLatency: keep submit -> verdict latencies of the most recent
+  // kLatencySamples items (off by default: a long-running node keeps none).
+  VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay, unsigned workers = 2,
+                     bool recordLatency = false);
   ~VerifyMicroBatcher();  // drains the queue, then stops the workers
   VerifyMicroBatcher(VerifyMicroBatcher const&) = delete;
   VerifyMicroBatcher& operator=(VerifyMicroBatcher const&) = delete;
 
-  // Thread-safe.  The future carries the verdict, or VerifyEngineError.
+  // Thread-safe.  The future carries the verdict.
   std::future<bool> submit(PublicKey const& key, Signature const& sig, ByteSlice const& msg);
+  // Thread-safe, fire and forget: the verdict lands in the verify cache only.
+  void post(PublicKey const& key, Signature const& sig, ByteSlice const& msg);
+  // Blocks until every item enqueued before the call has been verified.
+  void drain();
 
   struct Stats {
     uint64_t items = 0;
@@ -47,7 +57,9 @@ class VerifyMicroBatcher {
     uint64_t maxBatchSeen = 0;
   };
   Stats stats() const;
-  // submit -> verdict-ready latencies in microseconds (recorded per item)
+  static constexpr size_t kLatencySamples = 1 << 16;
+  // submit -> verdict-ready latencies in microseconds (recordLatency only;
+  // the most recent kLatencySamples items)
   std::vector<double> latencies() const;
 
  private:
@@ -55,19 +67,24 @@ class VerifyMicroBatcher {
     PublicKey key;
     Signature sig;
     std::vector<uint8_t> msg;
-    std::promise<bool> done;
+    std::unique_ptr<std::promise<bool>> done;  // submit() only
     std::chrono::steady_clock::time_point t0;
   };
+  void enqueue(Item&& it);
   void run();
 
   const size_t mMaxBatch;
   const std::chrono::microseconds mMaxDelay;
+  const bool mRecordLatency;
   mutable std::mutex mMu;
   std::condition_variable mCv;
+  std::condition_variable mDoneCv;
   std::deque<Item> mQueue;
   bool mStop = false;
+  uint64_t mEnqueued = 0, mCompleted = 0;
   Stats mStats;
-  std::vector<double> mLatUs;
+  std::vector<double> mLatUs;  // ring of kLatencySamples
+  size_t mLatNext = 0;
   std::vector<std::thread> mWorkers;
 };
 

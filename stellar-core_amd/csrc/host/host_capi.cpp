@@ -1,20 +1,21 @@
 // extern "C" surface of libstellar_host.so (the C++ PubKeyUtils /
-// SignatureChecker mirror), for bindings and tests.  Declared in
-// include/stellar_host.h.  C++ exceptions never cross this boundary.
+// SignatureChecker / transaction-signature mirror), for bindings and tests.
+// Declared in include/stellar_host.h.  C++ exceptions never cross this
+// boundary.
+#include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <exception>
+#include <future>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../../include/stellar_host.h"
 #include "PubKeyUtils.h"
 #include "SignatureChecker.h"
+#include "TransactionSignatures.h"
 #include "VerifyMicroBatcher.h"
-
-#include <algorithm>
-#include <chrono>
-#include <future>
-#include <thread>
 #include "hashes.h"
 
 using namespace stellar;
@@ -23,7 +24,38 @@ namespace {
 thread_local std::string t_err;
 int guard_exc(std::exception const& e) {
   t_err = e.what();
-  return dynamic_cast<VerifyEngineError const*>(&e) ? SVH_ERR_ENGINE : SVH_ERR_INVALID_ARG;
+  return SVH_ERR_INVALID_ARG;
+}
+
+DecoratedSignature decorated(svh_decorated_sig const& s) {
+  if (s.sig_len > 64) throw std::invalid_argument("signature longer than 64 bytes");
+  DecoratedSignature d;
+  std::memcpy(d.hint.data(), s.hint, 4);
+  d.signature.assign(s.sig, s.sig + s.sig_len);
+  return d;
+}
+
+Signer signer(svh_signer const& s) {
+  if (s.type > 3 || s.payload_len > 64) throw std::invalid_argument("bad signer");
+  Signer g;
+  g.key.type = (SignerKeyType)s.type;
+  std::memcpy(g.key.key.data(), s.key, 32);
+  g.key.payload.assign(s.payload, s.payload + s.payload_len);
+  g.weight = s.weight;
+  return g;
+}
+
+std::vector<DecoratedSignature> sigRange(const svh_decorated_sig* sigs, uint32_t off, uint32_t n) {
+  std::vector<DecoratedSignature> v;
+  v.reserve(n);
+  for (uint32_t k = 0; k < n; ++k) v.push_back(decorated(sigs[off + k]));
+  return v;
+}
+
+uint256 u256(const uint8_t* p) {
+  uint256 u;
+  std::memcpy(u.data(), p, 32);
+  return u;
 }
 }  // namespace
 
@@ -73,6 +105,16 @@ int svh_verify_sig_batch(const uint8_t* pk, const uint8_t* sig, const uint32_t* 
   }
 }
 
+int svh_verify_uncached(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                        const uint32_t* msg_len, size_t n, uint8_t* verdict) {
+  try {
+    PubKeyUtils::verifyBatchUncached(pk, sig, msg, msg_off, msg_len, n, verdict);
+    return SVH_OK;
+  } catch (std::exception const& e) {
+    return guard_exc(e);
+  }
+}
+
 void svh_cache_clear(void) { PubKeyUtils::clearVerifySigCache(); }
 void svh_cache_seed(unsigned int seed) { PubKeyUtils::maybeSeedVerifySigCache(seed); }
 void svh_cache_counts(uint64_t* hits, uint64_t* misses) {
@@ -81,15 +123,31 @@ void svh_cache_counts(uint64_t* hits, uint64_t* misses) {
   if (hits) *hits = h;
   if (misses) *misses = m;
 }
+size_t svh_cache_keys(uint8_t* out, size_t max_keys) {
+  auto keys = PubKeyUtils::cacheKeysForTesting();
+  const size_t n = std::min(max_keys, keys.size());
+  for (size_t i = 0; i < n; ++i) std::memcpy(out + 32 * i, keys[i].data(), 32);
+  return keys.size();
+}
 void svh_engine_counts(uint64_t* sigs, uint64_t* batches) {
   uint64_t s, b;
   PubKeyUtils::flushEngineCounts(s, b);
   if (sigs) *sigs = s;
   if (batches) *batches = b;
 }
+void svh_engine_counts_ex(svh_engine_stats* out) {
+  auto c = PubKeyUtils::flushEngineCounts();
+  if (out) {
+    out->gpu_signatures = c.gpuSignatures;
+    out->gpu_batches = c.gpuBatches;
+    out->cpu_signatures = c.cpuSignatures;
+    out->fallbacks = c.fallbacks;
+  }
+}
 void svh_set_test_verifier(svh_batch_verify_fn fn) { PubKeyUtils::setBatchVerifierForTesting(fn); }
 void svh_set_test_keyed_verifier(svh_keyed_verify_fn fn) { PubKeyUtils::setKeyedBatchVerifierForTesting(fn); }
 void svh_set_keyed_threshold(size_t min_items) { PubKeyUtils::setKeyedBatchThreshold(min_items); }
+void svh_set_cpu_threshold(size_t max_misses) { PubKeyUtils::setCpuBatchThreshold(max_misses); }
 
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs) {
@@ -99,29 +157,13 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
     std::vector<std::vector<Signer>> sgn(ntx);
     for (size_t t = 0; t < ntx; ++t) {
       std::memcpy(hashes[t].data(), txs[t].contents_hash, 32);
-      for (uint32_t k = 0; k < txs[t].nsigs; ++k) {
-        const svh_decorated_sig& s = sigs[txs[t].sig_off + k];
-        if (s.sig_len > 64) throw std::invalid_argument("signature longer than 64 bytes");
-        DecoratedSignature d;
-        std::memcpy(d.hint.data(), s.hint, 4);
-        d.signature.assign(s.sig, s.sig + s.sig_len);
-        dsigs[t].push_back(std::move(d));
-      }
-      for (uint32_t k = 0; k < txs[t].nsigners; ++k) {
-        const svh_signer& s = signers[txs[t].signer_off + k];
-        if (s.type > 3 || s.payload_len > 64) throw std::invalid_argument("bad signer");
-        Signer g;
-        g.key.type = (SignerKeyType)s.type;
-        std::memcpy(g.key.key.data(), s.key, 32);
-        g.key.payload.assign(s.payload, s.payload + s.payload_len);
-        g.weight = s.weight;
-        sgn[t].push_back(std::move(g));
-      }
+      dsigs[t] = sigRange(sigs, txs[t].sig_off, txs[t].nsigs);
+      for (uint32_t k = 0; k < txs[t].nsigners; ++k) sgn[t].push_back(signer(signers[txs[t].signer_off + k]));
     }
     SignatureBatchPrefetch pre;
     if (use_prefetch) {
       for (size_t t = 0; t < ntx; ++t) pre.add(hashes[t], dsigs[t], sgn[t]);
-      pre.run();
+      pre.run(use_prefetch == 2);
     }
     if (prefetched_pairs) *prefetched_pairs = pre.pairs();
     for (size_t t = 0; t < ntx; ++t) {
@@ -135,24 +177,91 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
   }
 }
 
-int svh_mb_run_workers(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
-                       const uint32_t* msg_len, size_t n, int producers, int workers, uint32_t max_batch,
-                       uint32_t max_delay_us, uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats) {
+int svh_check_envelopes(const svh_envelope* env, size_t n, const svh_decorated_sig* sigs, const svh_op* ops,
+                        const svh_signer* signers, const svh_account* accounts, size_t naccounts,
+                        uint32_t protocol, int prefetch, int for_apply, svh_tx_result* results,
+                        uint64_t* prefetched_pairs) {
+  try {
+    AccountSnapshot snap;
+    snap.reserve(naccounts);
+    for (size_t a = 0; a < naccounts; ++a) {
+      AccountSigState st;
+      st.accountID = u256(accounts[a].account_id);
+      std::memcpy(st.thresholds, accounts[a].thresholds, 4);
+      for (uint32_t k = 0; k < accounts[a].nsigners; ++k)
+        st.signers.push_back(signer(signers[accounts[a].signer_off + k]));
+      snap[st.accountID] = std::move(st);
+    }
+    std::vector<FeeBumpSigInfo> txs(n);
+    for (size_t t = 0; t < n; ++t) {
+      svh_envelope const& e = env[t];
+      TransactionSigInfo& in = txs[t].inner;
+      std::memcpy(in.contentsHash.data(), e.contents_hash, 32);
+      in.sourceAccount = u256(e.source);
+      in.signatures = sigRange(sigs, e.sig_off, e.nsigs);
+      for (uint32_t k = 0; k < e.nops; ++k) {
+        svh_op const& o = ops[e.op_off + k];
+        if (o.level < 1 || o.level > 3) throw std::invalid_argument("bad threshold level");
+        OperationSigInfo op;
+        if (o.has_source) op.sourceAccount = u256(o.source);
+        op.level = (ThresholdLevel)o.level;
+        in.operations.push_back(op);
+      }
+      for (uint32_t k = 0; k < e.nextra; ++k) in.extraSigners.push_back(signer(signers[e.extra_off + k]).key);
+      if (e.fee_bump) {
+        std::memcpy(txs[t].contentsHash.data(), e.fee_bump_hash, 32);
+        txs[t].feeSource = u256(e.fee_source);
+        txs[t].signatures = sigRange(sigs, e.outer_off, e.nouter);
+      }
+    }
+    SignatureBatchPrefetch pre;
+    if (prefetch) {
+      for (size_t t = 0; t < n; ++t) {
+        if (env[t].fee_bump) prefetchFeeBump(pre, txs[t], snap);
+        else prefetchTransaction(pre, txs[t].inner, snap);
+      }
+      pre.run(prefetch == 2);
+    }
+    if (prefetched_pairs) *prefetched_pairs = pre.pairs();
+    SignatureBatchPrefetch const* p = prefetch ? &pre : nullptr;
+    for (size_t t = 0; t < n; ++t) {
+      TxSigResult r = env[t].fee_bump ? checkFeeBumpSignatures(txs[t], snap, protocol, p, for_apply != 0)
+                                      : checkTransactionSignatures(txs[t].inner, snap, protocol, p, for_apply != 0);
+      results[t].code = r.code;
+      results[t].inner_code = r.innerCode;
+      results[t].failed_op = r.failedOp;
+      results[t].op_code = r.opCode;
+    }
+    return SVH_OK;
+  } catch (std::exception const& e) {
+    return guard_exc(e);
+  }
+}
+
+int svh_mb_run_ex(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                  const uint32_t* msg_len, size_t n, int producers, int workers, uint32_t max_batch,
+                  uint32_t max_delay_us, uint32_t inter_arrival_us, int fire_and_forget, uint8_t* verdict,
+                  svh_mb_stats* stats) {
   try {
     if (producers < 1) producers = 1;
     if (workers < 1) workers = 1;
     std::vector<int> err(producers, 0);
     std::vector<std::string> msgs(producers);
-    VerifyMicroBatcher mb(max_batch, std::chrono::microseconds(max_delay_us), (unsigned)workers);
+    VerifyMicroBatcher mb(max_batch, std::chrono::microseconds(max_delay_us), (unsigned)workers,
+                          /*recordLatency=*/!fire_and_forget);
+    const auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int p = 0; p < producers; ++p) {
       th.emplace_back([&, p] {
         std::vector<std::pair<size_t, std::future<bool>>> futs;
+        PublicKey k;
+        Signature s(64);
         for (size_t i = (size_t)p; i < n; i += (size_t)producers) {
-          PublicKey k;
           std::memcpy(k.ed25519().data(), pk + 32 * i, 32);
-          Signature s(sig + 64 * i, sig + 64 * i + 64);
-          futs.emplace_back(i, mb.submit(k, s, ByteSlice(msg + msg_off[i], msg_len[i])));
+          std::memcpy(s.data(), sig + 64 * i, 64);
+          const ByteSlice m(msg + msg_off[i], msg_len[i]);
+          if (fire_and_forget) mb.post(k, s, m);
+          else futs.emplace_back(i, mb.submit(k, s, m));
           if (inter_arrival_us) std::this_thread::sleep_for(std::chrono::microseconds(inter_arrival_us));
         }
         try {
@@ -164,11 +273,23 @@ int svh_mb_run_workers(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg
       });
     }
     for (auto& t : th) t.join();
+    if (fire_and_forget) mb.drain();
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     for (int p = 0; p < producers; ++p)
       if (err[p]) {
         t_err = msgs[p];
         return SVH_ERR_ENGINE;
       }
+    if (fire_and_forget && verdict) {
+      // the verdicts were only cached: read them back like the reference's
+      // later verifyEnvelope would (cache hits)
+      for (size_t i = 0; i < n; ++i) {
+        PublicKey k;
+        std::memcpy(k.ed25519().data(), pk + 32 * i, 32);
+        Signature s(sig + 64 * i, sig + 64 * i + 64);
+        verdict[i] = PubKeyUtils::verifySig(k, s, ByteSlice(msg + msg_off[i], msg_len[i])) ? 1 : 0;
+      }
+    }
     if (stats) {
       auto s = mb.stats();
       stats->items = s.items;
@@ -180,6 +301,7 @@ int svh_mb_run_workers(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg
       std::sort(lat.begin(), lat.end());
       stats->lat_p50_us = lat.empty() ? 0 : lat[lat.size() / 2];
       stats->lat_p99_us = lat.empty() ? 0 : lat[std::min(lat.size() - 1, (size_t)(lat.size() * 0.99))];
+      stats->wall_s = wall;
     }
     return SVH_OK;
   } catch (std::exception const& e) {
@@ -187,11 +309,18 @@ int svh_mb_run_workers(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg
   }
 }
 
+int svh_mb_run_workers(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                       const uint32_t* msg_len, size_t n, int producers, int workers, uint32_t max_batch,
+                       uint32_t max_delay_us, uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats) {
+  return svh_mb_run_ex(pk, sig, msg, msg_off, msg_len, n, producers, workers, max_batch, max_delay_us,
+                       inter_arrival_us, 0, verdict, stats);
+}
+
 int svh_mb_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                const uint32_t* msg_len, size_t n, int producers, uint32_t max_batch, uint32_t max_delay_us,
                uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats) {
-  return svh_mb_run_workers(pk, sig, msg, msg_off, msg_len, n, producers, 2, max_batch, max_delay_us,
-                            inter_arrival_us, verdict, stats);
+  return svh_mb_run_ex(pk, sig, msg, msg_off, msg_len, n, producers, 2, max_batch, max_delay_us, inter_arrival_us, 0,
+                       verdict, stats);
 }
 
 }  // extern "C"

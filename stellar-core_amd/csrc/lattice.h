@@ -218,7 +218,9 @@ SV_HD bool sv_lehmer_step(uint32_t a[8], uint32_t b[8], uint32_t ta[8], uint32_t
 }
 
 // h < L (8 words).  Always returns a valid pair (falls back to (h, 1)).
-SV_COLD void sc_lattice_reduce(sv_lat& o, const uint32_t h[8]) {
+// trivial (test knob, sv_set_debug_flags SV_DBG_TRIVIAL_PAIR): skip the
+// reduction and take the fallback pair (h, 1) -- the full-length equation.
+SV_COLD void sc_lattice_reduce(sv_lat& o, const uint32_t h[8], bool trivial = false) {
   uint32_t a[8], b[8], ta[8], tb[8];
   SV_UNROLL for (int i = 0; i < 8; ++i) {
     a[i] = sc_N8(i);
@@ -228,8 +230,8 @@ SV_COLD void sc_lattice_reduce(sv_lat& o, const uint32_t h[8]) {
   }
   tb[0] = 1;
   bool bneg = false;  // sign of t for b; t for a has the opposite sign
-  bool bail = false;
-  SV_NOUNROLL for (int it = 0; it < SV_LAT_MAX_ITERS; ++it) {
+  bool bail = trivial;
+  SV_NOUNROLL for (int it = 0; it < (trivial ? 0 : SV_LAT_MAX_ITERS); ++it) {
     uint32_t hi = 0;
     SV_UNROLL for (int i = SV_LAT_SPLIT_WORDS; i < 8; ++i) hi |= b[i];
     if (hi == 0) break;

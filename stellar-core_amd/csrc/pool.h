@@ -1,0 +1,99 @@
+// Persistent helper-thread pool shared by the engine's host side (staging,
+// multi-slot fan-out: sv_api.cpp) and the C++ mirror (parallel hashing and
+// CPU-path batches: host/).
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstddef>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace sv {
+
+// Persistent host threads for packing staging buffers and for driving several
+// device slots at once.  run(k, fn) executes fn(0..k-1); the calling thread
+// takes part and, while waiting, keeps executing queued tasks, so nested use
+// (a device slice that packs in parallel) cannot deadlock.
+class Pool {
+ public:
+  explicit Pool(unsigned threads) {
+    for (unsigned i = 0; i < threads; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  size_t size() const { return th_.size(); }
+  void run(size_t k, const std::function<void(size_t)>& fn) {
+    if (k == 0) return;
+    if (k == 1 || th_.empty()) {
+      for (size_t i = 0; i < k; ++i) fn(i);
+      return;
+    }
+    struct Group {
+      std::atomic<size_t> left;
+      std::mutex mu;
+      std::condition_variable cv;
+    } grp;
+    grp.left.store(k - 1);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (size_t i = 1; i < k; ++i)
+        q_.emplace_back([&grp, &fn, i] {
+          fn(i);
+          if (grp.left.fetch_sub(1) == 1) {
+            std::lock_guard<std::mutex> gg(grp.mu);
+            grp.cv.notify_all();
+          }
+        });
+    }
+    cv_.notify_all();
+    fn(0);
+    while (grp.left.load() != 0) {
+      std::function<void()> task;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (!q_.empty()) {
+          task = std::move(q_.front());
+          q_.pop_front();
+        }
+      }
+      if (task) {
+        task();
+        continue;
+      }
+      std::unique_lock<std::mutex> lk(grp.mu);
+      grp.cv.wait_for(lk, std::chrono::microseconds(200), [&] { return grp.left.load() == 0; });
+    }
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;
+      auto task = std::move(q_.front());
+      q_.pop_front();
+      lk.unlock();
+      task();
+      lk.lock();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false;
+};
+
+}  // namespace sv

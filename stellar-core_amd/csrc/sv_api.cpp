@@ -1,40 +1,60 @@
-// C-ABI implementation (include/stellar_sigverify.h): device discovery,
-// per-device resources, host<->device staging and multi-GPU sharding.
+// C-ABI implementation (include/stellar_sigverify.h): device slots, lazily
+// created per-slot resources, pipelined host<->device staging and multi-GPU
+// sharding.
 //
 // Replaces, for whole batches, the libsodium crypto_sign_verify_detached call
 // made by stellar::PubKeyUtils::verifySig on a verify-cache miss
 // (/root/reference/src/crypto/SecretKey.cpp:461-463).
 //
-// Per device: one non-blocking HIP stream, the 129-entry base-point table
-// (computed on the device at init), and the per-lane -A table workspace sized
-// for the persistent grid (CUs x resident workgroups).  All work for a device
-// is serialised on its stream under its mutex because the workspace is shared
-// by every launch on that device.  Multi-GPU: contiguous slices
-// [g*n/G, (g+1)*n/G), one host thread per device, verdicts copied back into
-// disjoint ranges of the caller's buffer -- no collective.
+// Device slots.  One slot per visible GPU by default; sv_set_device_map (or
+// the SV_DEVICE_MAP environment variable, e.g. "0,0") maps several logical
+// slots onto one physical GPU, which is how the multi-device code is tested
+// on a one-GPU box.  Per slot: three HIP streams (H2D copies, kernels, D2H
+// copies), the base-point tables (computed on the device at first use), and a
+// workspace allocated on the first throughput-path launch and sized to the
+// batch (the latency kernel needs none).  All work of a slot is serialised
+// under its mutex because the workspace is shared by every launch on it.
+//
+// Host buffers.  A host-buffer batch is cut into staging chunks (2^18
+// signatures by default); chunk c is packed into pinned slot c % 2 by the
+// helper pool, copied up on the H2D stream, verified on the kernel stream,
+// and its verdicts copied down on the D2H stream, so the packing and PCIe
+// copies of one chunk overlap the kernels of the previous one and a batch of
+// any size pins at most two chunks.
+//
+// Multi-GPU: contiguous slices [g*n/G, (g+1)*n/G) over G slots, G limited so
+// that every slice holds at least the minimum shard (2^16 signatures by
+// default: a 1k SCP batch stays on one GPU), driven by the persistent helper
+// pool; verdicts land in disjoint ranges of the caller's buffer -- no
+// collective.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/stellar_sigverify.h"
+#include "pool.h"
 
 extern "C" {
-size_t sv_ws_bytes_per_block(void);
-size_t sv_ws_bytes(unsigned grid);
+size_t sv_ws_bytes(unsigned grid, uint64_t cap);
+size_t sv_verify_ws_bytes(int path, unsigned grid, uint64_t n);
 size_t sv_btab_bytes(void);
 int sv_block_threads(void);
 hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s);
 int sv_occupancy_blocks_per_cu(void);
 hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, const void* sig, const void* msg,
                             const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n,
-                            void* verdict, void* bitmap, void* ws, const void* btab, hipStream_t s);
+                            void* verdict, void* bitmap, void* ws, const void* btab, uint32_t dbg, hipStream_t s);
 hipError_t sv_launch_sign(unsigned grid, const void* seed, const void* msg, uint64_t n, void* pk, void* sig,
                           void* ws, const void* btab, hipStream_t s);
 hipError_t sv_launch_hash(int kind, unsigned max_blocks, const void* pk, const void* sig, const void* msg,
@@ -59,6 +79,22 @@ int hip_fail(hipError_t e, const char* what) {
     if (_e != hipSuccess) return hip_fail(_e, #call);  \
   } while (0)
 
+size_t env_size(const char* name, size_t dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  char* end = nullptr;
+  const unsigned long long x = strtoull(v, &end, 0);
+  return (end && *end == 0) ? (size_t)x : dflt;
+}
+
+sv::Pool& pool() {
+  // The GPU box's share is 16 CPUs; the staging copies saturate well below.
+  static sv::Pool p((unsigned)std::min<size_t>(
+      env_size("SV_HOST_THREADS", std::min(8u, std::max(2u, std::thread::hardware_concurrency()))), 64));
+  return p;
+}
+
+// ------------------------------------------------------------ buffers
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -83,8 +119,7 @@ struct DevBuf {
   }
 };
 
-// Pinned host staging (hipHostMalloc): one H2D copy per batch instead of one
-// pageable copy per input array.
+// Pinned host staging (hipHostMalloc).
 struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -93,7 +128,7 @@ struct HostBuf {
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
-    const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+    const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 16);
     hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
     if (e != hipSuccess) {
       p = nullptr;
@@ -109,19 +144,29 @@ struct HostBuf {
   }
 };
 
+// One pinned + device staging slot of the host-buffer pipeline.
+struct Stage {
+  HostBuf h_in, h_out;
+  DevBuf d_in, d_verdict, d_keys;
+  hipEvent_t up = nullptr, done = nullptr, down = nullptr;
+  bool busy = false;  // a chunk's D2H is pending on `down`
+  size_t lo = 0, m = 0;
+};
+
 struct Device {
-  int id = -1;
+  int slot = -1;
+  int phys = -1;
   bool ready = false;  // resources created lazily on first use (under mu)
   int cus = 0;
   unsigned grid = 0;  // persistent grid (workgroups)
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr, h2d = nullptr, d2h = nullptr;
   void* btab = nullptr;
-  void* ws = nullptr;
+  DevBuf ws;  // kernel workspace, grown on demand (after draining `stream`)
   hipEvent_t dep_in = nullptr, dep_out = nullptr;
   std::mutex mu;
-  DevBuf pk, sig, msg, off, len, verdict, keys;
-  DevBuf in;          // staged batch: pk | sig | [off | len] | msg
-  HostBuf h_in, h_out;
+  Stage st[2];
+  DevBuf msg, off, len, keys;  // sha256 batches
+  HostBuf h_sha;
   // timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   std::vector<uint64_t> pending_n;
@@ -131,16 +176,29 @@ struct Device {
 
 std::mutex g_mu;
 std::vector<Device*> g_devs;
+std::vector<int> g_map;  // slot -> physical device (empty: identity)
 bool g_inited = false;
 std::atomic<int> g_timing{0};
-std::atomic<int> g_path{SV_PATH_AUTO};  // sv_set_kernel_path
+std::atomic<int> g_path{SV_PATH_AUTO};   // sv_set_kernel_path
+std::atomic<uint32_t> g_dbg{0};          // sv_set_debug_flags
+std::atomic<size_t> g_min_shard{0};      // sv_set_min_shard (0: default)
+std::atomic<uint64_t> g_rr{0};           // round-robin slot for single-slot calls
+
+constexpr uint32_t kKernelDbgMask = SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS;
 
 // Batches up to this size take the latency kernel under SV_PATH_AUTO
-// (measured crossover on MI355X, DESIGN.md section 3.5).
+// (measured crossover on MI355X, DESIGN.md section 3).
 constexpr uint64_t kQuickMax = 12288;
 
-// Kernel path for one launch: an explicit per-call request (sv_opts.flags),
-// else the process default, else by batch size.
+size_t min_shard() {
+  const size_t v = g_min_shard.load();
+  return v ? v : env_size("SV_MIN_SHARD", (size_t)1 << 16);
+}
+size_t stage_chunk() {
+  static const size_t c = std::max<size_t>(1024, env_size("SV_STAGE_CHUNK", (size_t)1 << 18));
+  return c;
+}
+
 int resolve_path(int requested, uint64_t n) {
   int p = requested != SV_PATH_AUTO ? requested : g_path.load();
   if (p == SV_PATH_AUTO) p = n <= kQuickMax ? SV_PATH_LATENCY : SV_PATH_THROUGHPUT;
@@ -152,49 +210,118 @@ int path_from_flags(uint32_t flags) {
   return SV_PATH_AUTO;
 }
 
-int init_device(Device& D, int id) {
-  D.id = id;
-  SV_HIP(hipSetDevice(id));
+int init_device(Device& D) {
+  SV_HIP(hipSetDevice(D.phys));
   hipDeviceProp_t prop;
-  SV_HIP(hipGetDeviceProperties(&prop, id));
+  SV_HIP(hipGetDeviceProperties(&prop, D.phys));
   D.cus = prop.multiProcessorCount;
   SV_HIP(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
+  SV_HIP(hipStreamCreateWithFlags(&D.h2d, hipStreamNonBlocking));
+  SV_HIP(hipStreamCreateWithFlags(&D.d2h, hipStreamNonBlocking));
   SV_HIP(hipEventCreateWithFlags(&D.dep_in, hipEventDisableTiming));
   SV_HIP(hipEventCreateWithFlags(&D.dep_out, hipEventDisableTiming));
+  for (Stage& s : D.st) {
+    SV_HIP(hipEventCreateWithFlags(&s.up, hipEventDisableTiming));
+    SV_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    SV_HIP(hipEventCreateWithFlags(&s.down, hipEventDisableTiming));
+  }
   SV_HIP(hipMalloc(&D.btab, sv_btab_bytes()));
   SV_HIP(sv_launch_btab_init((uint32_t*)D.btab, D.stream));
-  const int per_cu = sv_occupancy_blocks_per_cu();
-  D.grid = (unsigned)(D.cus * per_cu);
-  const size_t ws_bytes = sv_ws_bytes(D.grid);
-  hipError_t e = hipMalloc(&D.ws, ws_bytes);
-  if (e != hipSuccess) return fail(SV_ERR_ALLOC, std::string("workspace hipMalloc: ") + hipGetErrorString(e));
+  D.grid = (unsigned)(D.cus * sv_occupancy_blocks_per_cu());
   SV_HIP(hipStreamSynchronize(D.stream));
   return SV_OK;
 }
 
-// Enumerates devices only; per-device resources are created on first use so a
-// process that drives one GPU (one rank per GPU) never touches the others.
-int ensure_init() {
-  std::lock_guard<std::mutex> g(g_mu);
+void release_device(Device& D) {
+  if (!D.ready) return;
+  (void)hipSetDevice(D.phys);
+  (void)hipStreamSynchronize(D.stream);
+  (void)hipStreamSynchronize(D.h2d);
+  (void)hipStreamSynchronize(D.d2h);
+  for (auto& pr : D.pending) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  D.pending.clear();
+  D.pending_n.clear();
+  for (Stage& s : D.st) {
+    s.h_in.release(); s.h_out.release();
+    s.d_in.release(); s.d_verdict.release(); s.d_keys.release();
+    if (s.up) (void)hipEventDestroy(s.up);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.down) (void)hipEventDestroy(s.down);
+    s.up = s.done = s.down = nullptr;
+  }
+  D.msg.release(); D.off.release(); D.len.release(); D.keys.release(); D.h_sha.release();
+  D.ws.release();
+  if (D.btab) (void)hipFree(D.btab);
+  if (D.dep_in) (void)hipEventDestroy(D.dep_in);
+  if (D.dep_out) (void)hipEventDestroy(D.dep_out);
+  if (D.stream) (void)hipStreamDestroy(D.stream);
+  if (D.h2d) (void)hipStreamDestroy(D.h2d);
+  if (D.d2h) (void)hipStreamDestroy(D.d2h);
+  D.btab = nullptr;
+  D.stream = D.h2d = D.d2h = nullptr;
+  D.ready = false;
+}
+
+// Enumerates devices and builds the slot table; per-slot resources are
+// created on first use so a process that drives one GPU (one rank per GPU)
+// never touches the others.  Caller holds g_mu.
+int init_locked() {
   if (g_inited) return g_devs.empty() ? fail(SV_ERR_NO_DEVICE, "no HIP device") : SV_OK;
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
   g_inited = true;
   if (e != hipSuccess || n <= 0) return fail(SV_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
-  for (int i = 0; i < n; ++i) {
+  std::vector<int> map = g_map;
+  if (map.empty()) {
+    if (const char* env = getenv("SV_DEVICE_MAP")) {
+      const char* p = env;
+      while (*p) {
+        char* end = nullptr;
+        const long v = strtol(p, &end, 10);
+        if (end == p) break;
+        map.push_back((int)v);
+        p = *end == ',' ? end + 1 : end;
+      }
+    }
+  }
+  if (map.empty())
+    for (int i = 0; i < n; ++i) map.push_back(i);
+  for (int v : map)
+    if (v < 0 || v >= n) {
+      g_inited = false;
+      return fail(SV_ERR_INVALID_ARG, "device map names a device that does not exist");
+    }
+  for (size_t i = 0; i < map.size(); ++i) {
     Device* D = new Device();
-    D->id = i;
+    D->slot = (int)i;
+    D->phys = map[i];
     g_devs.push_back(D);
   }
   return SV_OK;
 }
 
+int ensure_init() {
+  std::lock_guard<std::mutex> g(g_mu);
+  return init_locked();
+}
+
 // Caller holds D.mu.
 int ready_locked(Device& D) {
   if (D.ready) return SV_OK;
-  int rc = init_device(D, D.id);
+  int rc = init_device(D);
   if (rc == SV_OK) D.ready = true;
   return rc;
+}
+
+// Workspace for a launch (caller holds D.mu, device set).  Growing it frees
+// the old one, so the kernel stream is drained first.
+int ensure_ws(Device& D, size_t bytes) {
+  if (bytes <= D.ws.cap) return SV_OK;
+  SV_HIP(hipStreamSynchronize(D.stream));
+  return D.ws.ensure(bytes);
 }
 
 unsigned grid_for(const Device& D, uint64_t n) {
@@ -205,6 +332,10 @@ unsigned grid_for(const Device& D, uint64_t n) {
 // Launch on D.stream (caller holds D.mu and has set the device).
 int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig, const void* msg, const uint64_t* off,
                   const uint32_t* len, uint32_t fixed_len, uint64_t n, void* verdict, void* bitmap) {
+  const int rp = resolve_path(path, n);
+  const unsigned grid = grid_for(D, n);
+  int rc;
+  if ((rc = ensure_ws(D, sv_verify_ws_bytes(rp, grid, n)))) return rc;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool timing = g_timing.load() != 0;
   if (timing) {
@@ -212,8 +343,8 @@ int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig
     SV_HIP(hipEventCreate(&e1));
     SV_HIP(hipEventRecord(e0, D.stream));
   }
-  SV_HIP(sv_launch_verify(mode, resolve_path(path, n), grid_for(D, n), pk, sig, msg, off, len, fixed_len, n, verdict,
-                          bitmap, D.ws, D.btab, D.stream));
+  SV_HIP(sv_launch_verify(mode, rp, grid, pk, sig, msg, off, len, fixed_len, n, verdict, bitmap, D.ws.p, D.btab,
+                          g_dbg.load() & kKernelDbgMask, D.stream));
   if (timing) {
     SV_HIP(hipEventRecord(e1, D.stream));
     D.pending.emplace_back(e0, e1);
@@ -238,181 +369,320 @@ int harvest_timing_locked(Device& D) {
   return SV_OK;
 }
 
-// Host-buffer slice on one device: stage once, then launch the verify kernel
-// (verdict != null) and/or the cache-key kernel (keys != null) on the same
-// stream, copy results back, sync.
-int host_slice(Device& D, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
-               const uint32_t* msg_len, uint32_t fixed_len, size_t n, uint8_t* verdict, uint8_t* keys, int path) {
-  std::lock_guard<std::mutex> g(D.mu);
-  SV_HIP(hipSetDevice(D.id));
-  int rc;
-  if ((rc = ready_locked(D))) return rc;
-  // one pinned staging image, one H2D copy:
-  //   pk (32 n) | sig (64 n) | fixed: msg (n L)  or  var: off (8 n) | len (4 n) | packed msgs
-  // (pk, sig, and a fixed-length msg block stay 16-byte aligned)
-  const size_t o_sig = 32 * n, o_var = 96 * n;
-  size_t total_msg = 0;
-  if (fixed_len != 0) {
-    total_msg = n * (size_t)fixed_len;
-  } else {
-    for (size_t i = 0; i < n; ++i) total_msg += msg_len[i];
+// ------------------------------------------------------------ host inputs
+// A batch in host memory: contiguous SoA arrays (pk n x 32, sig n x 64,
+// messages by offset/length or fixed stride), or pointer arrays (gather).
+struct HostIn {
+  const uint8_t* pk = nullptr;
+  const uint8_t* sig = nullptr;
+  const uint8_t* msg = nullptr;
+  const uint64_t* off = nullptr;
+  const uint32_t* len = nullptr;
+  uint32_t fixed = 0;  // != 0: message i = msg + i * fixed
+  const uint8_t* const* ppk = nullptr;  // gather form (ppk != nullptr)
+  const uint8_t* const* psig = nullptr;
+  const uint8_t* const* pmsg = nullptr;
+
+  bool gather() const { return ppk != nullptr; }
+  uint32_t mlen(size_t i) const { return fixed ? fixed : len[i]; }
+  const uint8_t* pkp(size_t i) const { return gather() ? ppk[i] : pk + 32 * i; }
+  const uint8_t* sigp(size_t i) const { return gather() ? psig[i] : sig + 64 * i; }
+  const uint8_t* msgp(size_t i) const {
+    if (gather()) return pmsg[i];
+    return fixed ? msg + i * (size_t)fixed : msg + off[i];
   }
-  const size_t o_off = o_var, o_len = o_var + 8 * n;
-  const size_t o_msg = fixed_len != 0 ? o_var : o_var + 12 * n;
-  const size_t bytes = o_msg + std::max<size_t>(total_msg, 1);
-  if ((rc = D.in.ensure(bytes)) || (rc = D.h_in.ensure(bytes))) return rc;
-  if (verdict && ((rc = D.verdict.ensure(n)) || (rc = D.h_out.ensure(n)))) return rc;
-  if (keys && (rc = D.keys.ensure(n * 32))) return rc;
-  uint8_t* h = (uint8_t*)D.h_in.p;
-  memcpy(h, pk, n * 32);
-  memcpy(h + o_sig, sig, n * 64);
-  int mode;
-  if (fixed_len != 0) {
-    if (total_msg) memcpy(h + o_msg, msg, total_msg);
-    mode = (fixed_len == 32) ? 0 : 2;
-  } else {
-    // pack this slice's messages contiguously (offsets may be arbitrary)
-    uint64_t* offs = (uint64_t*)(h + o_off);
-    size_t pos = 0;
-    for (size_t i = 0; i < n; ++i) {
-      offs[i] = pos;
-      if (msg_len[i]) memcpy(h + o_msg + pos, msg + msg_off[i], msg_len[i]);
-      pos += msg_len[i];
+  // the slice [lo, ...) as a batch of its own
+  HostIn sub(size_t lo) const {
+    HostIn s = *this;
+    if (gather()) {
+      s.ppk += lo;
+      s.psig += lo;
+      s.pmsg += lo;
+      s.len += lo;
+    } else {
+      s.pk += 32 * lo;
+      s.sig += 64 * lo;
+      if (fixed) s.msg += lo * (size_t)fixed;
+      else {
+        s.off += lo;
+        s.len += lo;
+      }
     }
-    memcpy(h + o_len, msg_len, n * 4);
-    mode = 1;
+    return s;
   }
-  SV_HIP(hipMemcpyAsync(D.in.p, h, bytes, hipMemcpyHostToDevice, D.stream));
-  uint8_t* d = (uint8_t*)D.in.p;
-  const uint64_t* d_off = fixed_len ? nullptr : (const uint64_t*)(d + o_off);
-  const uint32_t* d_len = fixed_len ? nullptr : (const uint32_t*)(d + o_len);
-  if (keys) {
-    SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + o_sig, d + o_msg, d_off, d_len, fixed_len, n, D.keys.p, D.stream));
-    SV_HIP(hipMemcpyAsync(keys, D.keys.p, n * 32, hipMemcpyDeviceToHost, D.stream));
+};
+
+// Pinned image of m signatures starting at `lo`:
+//   pk (32 m) | sig (64 m) | fixed: msgs (m L)   or   var: off (8 m) | len (4 m) | packed msgs
+// (pk, sig and a fixed-length message block stay 16-byte aligned).
+struct Image {
+  size_t o_sig, o_off, o_len, o_msg, bytes;
+  bool var;
+};
+
+Image image_of(const HostIn& in, size_t lo, size_t m, size_t* msg_total) {
+  Image im;
+  im.var = in.fixed == 0;
+  size_t total = 0;
+  if (!im.var) total = m * (size_t)in.fixed;
+  else
+    for (size_t i = 0; i < m; ++i) total += in.len[lo + i];
+  im.o_sig = 32 * m;
+  im.o_off = 96 * m;
+  im.o_len = im.o_off + 8 * m;
+  im.o_msg = im.var ? im.o_len + 4 * m : im.o_off;
+  im.bytes = im.o_msg + std::max<size_t>(total, 1);
+  *msg_total = total;
+  return im;
+}
+
+// Packs [lo, lo + m) into h (layout `im`), in parallel for large chunks.
+void pack(const HostIn& in, size_t lo, size_t m, const Image& im, uint8_t* h) {
+  uint64_t* offs = (uint64_t*)(h + im.o_off);
+  if (im.var) {
+    uint64_t pos = 0;
+    for (size_t i = 0; i < m; ++i) {
+      offs[i] = pos;
+      pos += in.len[lo + i];
+    }
   }
-  if (verdict) {
-    if ((rc = launch_locked(D, mode, path, d, d + o_sig, d + o_msg, d_off, d_len, fixed_len, n, D.verdict.p,
-                            nullptr)))
-      return rc;
-    SV_HIP(hipMemcpyAsync(D.h_out.p, D.verdict.p, n, hipMemcpyDeviceToHost, D.stream));
-  }
-  SV_HIP(hipStreamSynchronize(D.stream));  // the staging buffers are reused by the next call
-  if (verdict) memcpy(verdict, D.h_out.p, n);
+  const size_t kPart = 1u << 20;  // bytes per helper task
+  const size_t parts = std::max<size_t>(1, std::min<size_t>(pool().size() + 1, im.bytes / kPart));
+  pool().run(parts, [&](size_t t) {
+    const size_t a = m * t / parts, b = m * (t + 1) / parts;
+    if (a == b) return;
+    if (!in.gather()) {
+      std::memcpy(h + 32 * a, in.pk + 32 * (lo + a), 32 * (b - a));
+      std::memcpy(h + im.o_sig + 64 * a, in.sig + 64 * (lo + a), 64 * (b - a));
+      if (!im.var) {
+        std::memcpy(h + im.o_msg + a * (size_t)in.fixed, in.msg + (lo + a) * (size_t)in.fixed,
+                    (b - a) * (size_t)in.fixed);
+        return;
+      }
+    } else {
+      for (size_t i = a; i < b; ++i) {
+        std::memcpy(h + 32 * i, in.ppk[lo + i], 32);
+        std::memcpy(h + im.o_sig + 64 * i, in.psig[lo + i], 64);
+      }
+      if (!im.var) {
+        for (size_t i = a; i < b; ++i)
+          std::memcpy(h + im.o_msg + i * (size_t)in.fixed, in.pmsg[lo + i], in.fixed);
+        return;
+      }
+    }
+    std::memcpy(h + im.o_len + 4 * a, in.len + lo + a, 4 * (b - a));
+    for (size_t i = a; i < b; ++i) {
+      const uint32_t l = in.len[lo + i];
+      if (l) std::memcpy(h + im.o_msg + offs[i], in.msgp(lo + i), l);
+    }
+  });
+}
+
+// Collects a finished chunk's results from its pinned slot.
+int drain_stage(Stage& s, uint8_t* verdict, uint8_t* keys) {
+  if (!s.busy) return SV_OK;
+  SV_HIP(hipEventSynchronize(s.down));
+  s.busy = false;
+  const uint8_t* h = (const uint8_t*)s.h_out.p;
+  if (verdict) std::memcpy(verdict + s.lo, h, s.m);
+  if (keys) std::memcpy(keys + 32 * s.lo, h + (verdict ? s.m : 0), 32 * s.m);
   return SV_OK;
 }
 
-// SHA-256 of a host slice of byte strings on one device.
-int sha_slice(Device& D, const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t fixed_len,
-              size_t n, uint8_t* out) {
+// Host-buffer slice on one slot, pipelined over staging chunks: verdicts
+// (verdict != null) and/or BLAKE2b cache keys (keys != null) into the
+// caller's arrays.
+int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, int path) {
+  const size_t chunk = std::min(n, stage_chunk());
+  int rc;
+  // the largest launch first, so the workspace never grows under a running kernel
+  if (verdict && (rc = ensure_ws(D, sv_verify_ws_bytes(resolve_path(path, chunk), grid_for(D, chunk), chunk))))
+    return rc;
+  const size_t out_per = (verdict ? 1 : 0) + (keys ? 32 : 0);
+  size_t c = 0;
+  for (size_t lo = 0; lo < n; lo += chunk, ++c) {
+    Stage& s = D.st[c & 1];
+    // slot c & 1 was last used by chunk c - 2: its results are collected
+    // (which also means its H2D, kernels and D2H are complete)
+    if ((rc = drain_stage(s, verdict, keys))) return rc;
+    const size_t m = std::min(chunk, n - lo);
+    size_t msg_total;
+    const Image im = image_of(in, lo, m, &msg_total);
+    if ((rc = s.h_in.ensure(im.bytes)) || (rc = s.d_in.ensure(im.bytes)) || (rc = s.h_out.ensure(out_per * m)))
+      return rc;
+    if (verdict && (rc = s.d_verdict.ensure(m))) return rc;
+    if (keys && (rc = s.d_keys.ensure(32 * m))) return rc;
+    pack(in, lo, m, im, (uint8_t*)s.h_in.p);
+    SV_HIP(hipMemcpyAsync(s.d_in.p, s.h_in.p, im.bytes, hipMemcpyHostToDevice, D.h2d));
+    SV_HIP(hipEventRecord(s.up, D.h2d));
+    SV_HIP(hipStreamWaitEvent(D.stream, s.up, 0));
+    uint8_t* d = (uint8_t*)s.d_in.p;
+    const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
+    const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
+    if (keys)
+      SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m, s.d_keys.p,
+                            D.stream));
+    if (verdict) {
+      const int mode = im.var ? 1 : (in.fixed == 32 ? 0 : 2);
+      if ((rc = launch_locked(D, mode, path, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m,
+                              s.d_verdict.p, nullptr)))
+        return rc;
+    }
+    SV_HIP(hipEventRecord(s.done, D.stream));
+    SV_HIP(hipStreamWaitEvent(D.d2h, s.done, 0));
+    uint8_t* ho = (uint8_t*)s.h_out.p;
+    if (verdict) SV_HIP(hipMemcpyAsync(ho, s.d_verdict.p, m, hipMemcpyDeviceToHost, D.d2h));
+    if (keys) SV_HIP(hipMemcpyAsync(ho + (verdict ? m : 0), s.d_keys.p, 32 * m, hipMemcpyDeviceToHost, D.d2h));
+    SV_HIP(hipEventRecord(s.down, D.d2h));
+    s.busy = true;
+    s.lo = lo;
+    s.m = m;
+  }
+  for (Stage& s : D.st)
+    if ((rc = drain_stage(s, verdict, keys))) return rc;
+  return SV_OK;
+}
+
+int host_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, int path) {
   std::lock_guard<std::mutex> g(D.mu);
-  SV_HIP(hipSetDevice(D.id));
+  SV_HIP(hipSetDevice(D.phys));
   int rc;
   if ((rc = ready_locked(D))) return rc;
-  if ((rc = D.keys.ensure(n * 32))) return rc;
-  std::vector<uint64_t> offs;
-  std::vector<uint8_t> packed;
-  if (fixed_len != 0) {
-    if ((rc = D.msg.ensure((size_t)n * fixed_len))) return rc;
-    SV_HIP(hipMemcpyAsync(D.msg.p, data, n * (size_t)fixed_len, hipMemcpyHostToDevice, D.stream));
-  } else {
-    size_t total = 0;
-    for (size_t i = 0; i < n; ++i) total += len[i];
-    packed.resize(std::max<size_t>(total, 1));
-    offs.resize(n);
-    size_t pos = 0;
-    for (size_t i = 0; i < n; ++i) {
-      offs[i] = pos;
-      if (len[i]) memcpy(packed.data() + pos, data + off[i], len[i]);
-      pos += len[i];
-    }
-    if ((rc = D.msg.ensure(packed.size())) || (rc = D.off.ensure(n * 8)) || (rc = D.len.ensure(n * 4))) return rc;
-    SV_HIP(hipMemcpyAsync(D.msg.p, packed.data(), packed.size(), hipMemcpyHostToDevice, D.stream));
-    SV_HIP(hipMemcpyAsync(D.off.p, offs.data(), n * 8, hipMemcpyHostToDevice, D.stream));
-    SV_HIP(hipMemcpyAsync(D.len.p, len, n * 4, hipMemcpyHostToDevice, D.stream));
+  rc = host_slice_locked(D, in, n, verdict, keys, path);
+  if (rc != SV_OK) {
+    // leave the slot reusable: nothing of this call may still be in flight
+    (void)hipStreamSynchronize(D.h2d);
+    (void)hipStreamSynchronize(D.stream);
+    (void)hipStreamSynchronize(D.d2h);
+    D.st[0].busy = D.st[1].busy = false;
   }
-  SV_HIP(sv_launch_hash(1, D.grid * 2, nullptr, nullptr, D.msg.p, (const uint64_t*)D.off.p,
-                        (const uint32_t*)D.len.p, fixed_len, n, D.keys.p, D.stream));
+  return rc;
+}
+
+// SHA-256 of a host slice of byte strings on one slot.
+int sha_slice(Device& D, const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n, uint8_t* out) {
+  std::lock_guard<std::mutex> g(D.mu);
+  SV_HIP(hipSetDevice(D.phys));
+  int rc;
+  if ((rc = ready_locked(D))) return rc;
+  size_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += len[i];
+  const size_t o_len = 8 * n, o_msg = 12 * n, bytes = o_msg + std::max<size_t>(total, 1);
+  if ((rc = D.h_sha.ensure(bytes)) || (rc = D.msg.ensure(bytes)) || (rc = D.keys.ensure(n * 32))) return rc;
+  uint8_t* h = (uint8_t*)D.h_sha.p;
+  uint64_t* offs = (uint64_t*)h;
+  size_t pos = 0;
+  for (size_t i = 0; i < n; ++i) {
+    offs[i] = pos;
+    if (len[i]) std::memcpy(h + o_msg + pos, data + off[i], len[i]);
+    pos += len[i];
+  }
+  std::memcpy(h + o_len, len, 4 * n);
+  SV_HIP(hipMemcpyAsync(D.msg.p, h, bytes, hipMemcpyHostToDevice, D.stream));
+  uint8_t* d = (uint8_t*)D.msg.p;
+  SV_HIP(sv_launch_hash(1, D.grid * 2, nullptr, nullptr, d + o_msg, (const uint64_t*)d, (const uint32_t*)(d + o_len),
+                        0, n, D.keys.p, D.stream));
   SV_HIP(hipMemcpyAsync(out, D.keys.p, n * 32, hipMemcpyDeviceToHost, D.stream));
   SV_HIP(hipStreamSynchronize(D.stream));
   return SV_OK;
 }
 
-int select_devices(const sv_opts* opts, std::vector<Device*>& out) {
-  int dev = -1;
-  uint32_t maxd = 0;
-  if (opts) {
-    if (opts->struct_size < sizeof(sv_opts) || (opts->flags & ~SV_FLAG_PATH_MASK) != 0 ||
-        (opts->flags & SV_FLAG_PATH_MASK) == SV_FLAG_PATH_MASK)
-      return fail(SV_ERR_INVALID_ARG, "bad sv_opts");
-    dev = opts->device;
-    maxd = opts->max_devices;
-  }
-  if (dev >= 0) {
-    if (dev >= (int)g_devs.size()) return fail(SV_ERR_INVALID_ARG, "device index out of range");
-    out.push_back(g_devs[dev]);
-  } else {
-    for (Device* d : g_devs) {
-      if (maxd && out.size() >= maxd) break;
-      out.push_back(d);
-    }
-  }
+int check_opts(const sv_opts* opts) {
+  if (opts && (opts->struct_size < sizeof(sv_opts) || (opts->flags & ~SV_FLAG_PATH_MASK) != 0 ||
+               (opts->flags & SV_FLAG_PATH_MASK) == SV_FLAG_PATH_MASK))
+    return fail(SV_ERR_INVALID_ARG, "bad sv_opts");
   return SV_OK;
 }
 
-// Runs fn(device, lo, hi) for contiguous slices [g*n/G, (g+1)*n/G), one host
-// thread per device; the first failing device's error is reported.
+// The slots a host-buffer batch of n runs on: one named slot, or contiguous
+// slices over up to max_devices slots, each slice >= the minimum shard.
+int select_devices(const sv_opts* opts, size_t n, std::vector<Device*>& out) {
+  int rc;
+  if ((rc = check_opts(opts))) return rc;
+  const int dev = opts ? opts->device : -1;
+  const uint32_t maxd = opts ? opts->max_devices : 0;
+  if (dev >= 0) {
+    if (dev >= (int)g_devs.size()) return fail(SV_ERR_INVALID_ARG, "device index out of range");
+    out.push_back(g_devs[dev]);
+    return SV_OK;
+  }
+  size_t G = g_devs.size();
+  if (maxd) G = std::min<size_t>(G, maxd);
+  G = std::max<size_t>(1, std::min<size_t>(G, n / std::max<size_t>(1, min_shard())));
+  if (G == 1) {
+    // single-slot calls rotate over the slots so concurrent callers spread out
+    const size_t pool_n = maxd ? std::min<size_t>(g_devs.size(), maxd) : g_devs.size();
+    out.push_back(g_devs[(size_t)(g_rr.fetch_add(1) % pool_n)]);
+    return SV_OK;
+  }
+  for (size_t g = 0; g < G; ++g) out.push_back(g_devs[g]);
+  return SV_OK;
+}
+
+// Runs fn(slot, lo, hi) for contiguous slices [g*n/G, (g+1)*n/G) on the
+// helper pool; the first failing slot's error is reported.
 template <class F>
 int shard(const std::vector<Device*>& devs, size_t n, F fn) {
   const size_t G = devs.size();
   if (G == 1) return fn(*devs[0], (size_t)0, n);
   std::vector<int> rcs(G, SV_OK);
   std::vector<std::string> errs(G);
-  std::vector<std::thread> th;
-  for (size_t g = 0; g < G; ++g) {
+  pool().run(G, [&](size_t g) {
     const size_t lo = g * n / G, hi = (g + 1) * n / G;
-    if (hi == lo) continue;
-    th.emplace_back([&, g, lo, hi] {
-      rcs[g] = fn(*devs[g], lo, hi);
-      if (rcs[g]) errs[g] = t_err;
-    });
-  }
-  for (auto& t : th) t.join();
+    if (hi == lo) return;
+    rcs[g] = fn(*devs[g], lo, hi);
+    if (rcs[g]) errs[g] = t_err;
+  });
   for (size_t g = 0; g < G; ++g)
-    if (rcs[g]) return fail(rcs[g], "device " + std::to_string(devs[g]->id) + ": " + errs[g]);
+    if (rcs[g]) return fail(rcs[g], "device slot " + std::to_string(devs[g]->slot) + ": " + errs[g]);
   return SV_OK;
 }
 
-int check_msgs(const uint8_t* msg, const uint64_t* msg_off, const uint32_t* msg_len, uint32_t fixed_len, size_t n) {
-  if (fixed_len == 0 && (!msg_off || !msg_len)) return fail(SV_ERR_INVALID_ARG, "null msg_off/msg_len");
-  if (!msg) {
-    bool any = false;
-    if (fixed_len) any = true;
-    else
-      for (size_t i = 0; i < n && !any; ++i) any = msg_len[i] != 0;
+int check_msgs(const HostIn& in, size_t n) {
+  if (in.gather()) {
+    if (!in.psig || !in.len) return fail(SV_ERR_INVALID_ARG, "null pointer array");
+    for (size_t i = 0; i < n; ++i)
+      if (!in.ppk[i] || !in.psig[i] || (in.len[i] && (!in.pmsg || !in.pmsg[i])))
+        return fail(SV_ERR_INVALID_ARG, "null item pointer");
+    return SV_OK;
+  }
+  if (!in.pk || !in.sig) return fail(SV_ERR_INVALID_ARG, "null buffer");
+  if (in.fixed == 0 && (!in.off || !in.len)) return fail(SV_ERR_INVALID_ARG, "null msg_off/msg_len");
+  if (!in.msg) {
+    bool any = in.fixed != 0;
+    for (size_t i = 0; i < n && !any; ++i) any = in.len[i] != 0;
     if (any) return fail(SV_ERR_INVALID_ARG, "null msg");
   }
   return SV_OK;
 }
 
-int verify_host(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
-                const uint32_t* msg_len, uint32_t fixed_len, size_t n, uint8_t* verdict, uint8_t* keys,
-                const sv_opts* opts) {
-  if (n == 0) return SV_OK;
-  if (!pk || !sig || (!verdict && !keys)) return fail(SV_ERR_INVALID_ARG, "null buffer");
-  int rc = check_msgs(msg, msg_off, msg_len, fixed_len, n);
+int debug_fail() {
+  if (g_dbg.load() & SV_DBG_FAIL) return fail(SV_ERR_HIP, "injected device error (sv_set_debug_flags SV_DBG_FAIL)");
+  return SV_OK;
+}
+
+int verify_host(const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, const sv_opts* opts) {
+  if (n == 0) return check_opts(opts);
+  if (!verdict && !keys) return fail(SV_ERR_INVALID_ARG, "null buffer");
+  int rc = check_msgs(in, n);
   if (rc) return rc;
+  if ((rc = debug_fail())) return rc;
   if ((rc = ensure_init())) return rc;
   std::vector<Device*> devs;
-  if ((rc = select_devices(opts, devs))) return rc;
+  if ((rc = select_devices(opts, n, devs))) return rc;
+  const int path = path_from_flags(opts ? opts->flags : 0u);
   return shard(devs, n, [&](Device& D, size_t lo, size_t hi) {
-    return host_slice(D, pk + 32 * lo, sig + 64 * lo, fixed_len ? msg + lo * (size_t)fixed_len : msg,
-                      fixed_len ? nullptr : msg_off + lo, fixed_len ? nullptr : msg_len + lo, fixed_len, hi - lo,
-                      verdict ? verdict + lo : nullptr, keys ? keys + 32 * lo : nullptr,
-                      path_from_flags(opts ? opts->flags : 0u));
+    return host_slice(D, in.sub(lo), hi - lo, verdict ? verdict + lo : nullptr, keys ? keys + 32 * lo : nullptr,
+                      path);
   });
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+Device* device_arg(int device) {
+  if (device < 0 || device >= (int)g_devs.size()) return nullptr;
+  return g_devs[device];
+}
 
 }  // namespace
 
@@ -424,25 +694,26 @@ void sv_shutdown(void) {
   std::lock_guard<std::mutex> g(g_mu);
   for (Device* D : g_devs) {
     std::lock_guard<std::mutex> gd(D->mu);
-    if (!D->ready) continue;
-    (void)hipSetDevice(D->id);
-    (void)hipStreamSynchronize(D->stream);
-    for (auto& pr : D->pending) {
-      (void)hipEventDestroy(pr.first);
-      (void)hipEventDestroy(pr.second);
-    }
-    D->pk.release(); D->sig.release(); D->msg.release();
-    D->off.release(); D->len.release(); D->verdict.release(); D->keys.release();
-    D->in.release(); D->h_in.release(); D->h_out.release();
-    if (D->ws) (void)hipFree(D->ws);
-    if (D->btab) (void)hipFree(D->btab);
-    if (D->dep_in) (void)hipEventDestroy(D->dep_in);
-    if (D->dep_out) (void)hipEventDestroy(D->dep_out);
-    if (D->stream) (void)hipStreamDestroy(D->stream);
+    release_device(*D);
   }
   for (Device* D : g_devs) delete D;
   g_devs.clear();
   g_inited = false;
+}
+
+int sv_set_device_map(const int* physical, int count) {
+  if (count < 0 || (count > 0 && !physical)) return fail(SV_ERR_INVALID_ARG, "bad device map");
+  sv_shutdown();
+  std::lock_guard<std::mutex> g(g_mu);
+  g_map.assign(physical, physical + count);
+  int rc = init_locked();
+  if (rc != SV_OK) {
+    for (Device* D : g_devs) delete D;
+    g_devs.clear();
+    g_map.clear();
+    g_inited = false;
+  }
+  return rc;
 }
 
 int sv_device_count(void) {
@@ -454,12 +725,18 @@ int sv_device_count(void) {
 const char* sv_last_error_string(void) { return t_err.c_str(); }
 
 const char* sv_version(void) {
-  return "stellar-core_amd sigverify r1 (gfx950; ed25519 == libsodium-1.0.18 crypto_sign_verify_detached)";
+  return "stellar-core_amd sigverify r2 (gfx950; ed25519 == libsodium-1.0.18 crypto_sign_verify_detached)";
 }
 
 int sv_ed25519_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                             const uint32_t* msg_len, size_t n, uint8_t* verdict, const sv_opts* opts) {
-  return verify_host(pk, sig, msg, msg_off, msg_len, 0, n, verdict, nullptr, opts);
+  HostIn in;
+  in.pk = pk;
+  in.sig = sig;
+  in.msg = msg;
+  in.off = msg_off;
+  in.len = msg_len;
+  return verify_host(in, n, verdict, nullptr, opts);
 }
 
 int sv_ed25519_verify_batch_fixed(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_len,
@@ -469,35 +746,71 @@ int sv_ed25519_verify_batch_fixed(const uint8_t* pk, const uint8_t* sig, const u
     std::vector<uint64_t> off(n, 0);
     std::vector<uint32_t> len(n, 0);
     static const uint8_t dummy = 0;
-    return verify_host(pk, sig, &dummy, off.data(), len.data(), 0, n, verdict, nullptr, opts);
+    return sv_ed25519_verify_batch(pk, sig, &dummy, off.data(), len.data(), n, verdict, opts);
   }
-  return verify_host(pk, sig, msg, nullptr, nullptr, msg_len, n, verdict, nullptr, opts);
+  HostIn in;
+  in.pk = pk;
+  in.sig = sig;
+  in.msg = msg;
+  in.fixed = msg_len;
+  return verify_host(in, n, verdict, nullptr, opts);
+}
+
+int sv_ed25519_verify_batch_gather(const uint8_t* const* pk, const uint8_t* const* sig, const uint8_t* const* msg,
+                                   const uint32_t* msg_len, size_t n, uint8_t* verdict, uint8_t* keys,
+                                   const sv_opts* opts) {
+  if (n && (!pk || !verdict)) return fail(SV_ERR_INVALID_ARG, "null buffer");
+  HostIn in;
+  in.ppk = pk;
+  in.psig = sig;
+  in.pmsg = msg;
+  in.len = msg_len;
+  return verify_host(in, n, verdict, keys, opts);
 }
 
 int sv_ed25519_verify_batch_keyed(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                                   const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* verdict,
                                   uint8_t* keys, const sv_opts* opts) {
   if (!verdict || !keys) return n ? fail(SV_ERR_INVALID_ARG, "null verdict/keys") : SV_OK;
-  return verify_host(pk, sig, msg, msg_off, msg_len, 0, n, verdict, keys, opts);
+  HostIn in;
+  in.pk = pk;
+  in.sig = sig;
+  in.msg = msg;
+  in.off = msg_off;
+  in.len = msg_len;
+  return verify_host(in, n, verdict, keys, opts);
 }
 
 int sv_verify_cache_keys(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                          const uint32_t* msg_len, size_t n, uint8_t* keys, const sv_opts* opts) {
   if (!keys) return n ? fail(SV_ERR_INVALID_ARG, "null keys") : SV_OK;
-  return verify_host(pk, sig, msg, msg_off, msg_len, 0, n, nullptr, keys, opts);
+  HostIn in;
+  in.pk = pk;
+  in.sig = sig;
+  in.msg = msg;
+  in.off = msg_off;
+  in.len = msg_len;
+  return verify_host(in, n, nullptr, keys, opts);
 }
 
 int sv_sha256_batch(const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n, uint8_t* digests,
                     const sv_opts* opts) {
-  if (n == 0) return SV_OK;
+  if (n == 0) return check_opts(opts);
   if (!digests) return fail(SV_ERR_INVALID_ARG, "null digests");
-  int rc = check_msgs(data, off, len, 0, n);
+  HostIn in;
+  in.pk = data;  // (only the message fields are checked / used)
+  in.sig = data;
+  in.msg = data;
+  in.off = off;
+  in.len = len;
+  int rc = check_msgs(in, n);
   if (rc) return rc;
+  if ((rc = debug_fail())) return rc;
   if ((rc = ensure_init())) return rc;
   std::vector<Device*> devs;
-  if ((rc = select_devices(opts, devs))) return rc;
+  if ((rc = select_devices(opts, n, devs))) return rc;
   return shard(devs, n, [&](Device& D, size_t lo, size_t hi) {
-    return sha_slice(D, data, off + lo, len + lo, 0, hi - lo, digests + 32 * lo);
+    return sha_slice(D, data, off + lo, len + lo, hi - lo, digests + 32 * lo);
   });
 }
 
@@ -507,15 +820,17 @@ static int hash_device(int kind, int device, const void* d_pk, const void* d_sig
                        void* stream) {
   int rc = ensure_init();
   if (rc) return rc;
-  if (device < 0 || device >= (int)g_devs.size()) return fail(SV_ERR_INVALID_ARG, "device index out of range");
+  Device* Dp = device_arg(device);
+  if (!Dp) return fail(SV_ERR_INVALID_ARG, "device index out of range");
   if (n == 0) return SV_OK;
   if (!d_out || !d_msg || (kind == 0 && (!d_pk || !d_sig))) return fail(SV_ERR_INVALID_ARG, "null device buffer");
   if (fixed_len == 0 && (!d_off || !d_len)) return fail(SV_ERR_INVALID_ARG, "null msg_off/msg_len");
   if ((((uintptr_t)d_out) & 3u) || (kind == 0 && ((((uintptr_t)d_pk) & 3u) || (((uintptr_t)d_sig) & 3u))))
     return fail(SV_ERR_ALIGN, "pk/sig/out must be 4-byte aligned");
-  Device& D = *g_devs[device];
+  if ((rc = debug_fail())) return rc;
+  Device& D = *Dp;
   std::lock_guard<std::mutex> g(D.mu);
-  SV_HIP(hipSetDevice(D.id));
+  SV_HIP(hipSetDevice(D.phys));
   if ((rc = ready_locked(D))) return rc;
   hipStream_t user = (hipStream_t)stream;
   SV_HIP(hipEventRecord(D.dep_in, user));
@@ -542,7 +857,8 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
                              size_t n, void* d_verdict, void* d_bitmap, void* stream) {
   int rc = ensure_init();
   if (rc) return rc;
-  if (device < 0 || device >= (int)g_devs.size()) return fail(SV_ERR_INVALID_ARG, "device index out of range");
+  Device* Dp = device_arg(device);
+  if (!Dp) return fail(SV_ERR_INVALID_ARG, "device index out of range");
   if (n == 0) return SV_OK;
   if (!d_pk || !d_sig || !d_verdict) return fail(SV_ERR_INVALID_ARG, "null device buffer");
   if (!aligned16(d_pk) || !aligned16(d_sig)) return fail(SV_ERR_ALIGN, "pk/sig must be 16-byte aligned");
@@ -554,9 +870,10 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
     mode = 1;
   }
   if (!d_msg) return fail(SV_ERR_INVALID_ARG, "null msg");
-  Device& D = *g_devs[device];
+  if ((rc = debug_fail())) return rc;
+  Device& D = *Dp;
   std::lock_guard<std::mutex> g(D.mu);
-  SV_HIP(hipSetDevice(D.id));
+  SV_HIP(hipSetDevice(D.phys));
   if ((rc = ready_locked(D))) return rc;
   hipStream_t user = (hipStream_t)stream;
   SV_HIP(hipEventRecord(D.dep_in, user));
@@ -574,23 +891,36 @@ int sv_set_kernel_path(int path) {
   return g_path.exchange(path);
 }
 
+int sv_set_debug_flags(uint32_t flags) {
+  if (flags & ~(SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_FAIL)) return SV_ERR_INVALID_ARG;
+  return (int)g_dbg.exchange(flags);
+}
+
+int sv_set_min_shard(size_t n) {
+  g_min_shard.store(n);
+  return SV_OK;
+}
+
 int sv_ed25519_sign_device(int device, const void* d_seed, const void* d_msg32, size_t n, void* d_pk, void* d_sig,
                            void* stream) {
   int rc = ensure_init();
   if (rc) return rc;
-  if (device < 0 || device >= (int)g_devs.size()) return fail(SV_ERR_INVALID_ARG, "device index out of range");
+  Device* Dp = device_arg(device);
+  if (!Dp) return fail(SV_ERR_INVALID_ARG, "device index out of range");
   if (n == 0) return SV_OK;
   if (!d_seed || !d_msg32 || !d_pk || !d_sig) return fail(SV_ERR_INVALID_ARG, "null device buffer");
   if (!aligned16(d_seed) || !aligned16(d_msg32) || !aligned16(d_pk) || !aligned16(d_sig))
     return fail(SV_ERR_ALIGN, "buffers must be 16-byte aligned");
-  Device& D = *g_devs[device];
+  Device& D = *Dp;
   std::lock_guard<std::mutex> g(D.mu);
-  SV_HIP(hipSetDevice(D.id));
+  SV_HIP(hipSetDevice(D.phys));
   if ((rc = ready_locked(D))) return rc;
+  const unsigned grid = grid_for(D, n);
+  if ((rc = ensure_ws(D, sv_ws_bytes(grid, 0)))) return rc;
   hipStream_t user = (hipStream_t)stream;
   SV_HIP(hipEventRecord(D.dep_in, user));
   SV_HIP(hipStreamWaitEvent(D.stream, D.dep_in, 0));
-  SV_HIP(sv_launch_sign(grid_for(D, n), d_seed, d_msg32, n, d_pk, d_sig, D.ws, D.btab, D.stream));
+  SV_HIP(sv_launch_sign(grid, d_seed, d_msg32, n, d_pk, d_sig, D.ws.p, D.btab, D.stream));
   SV_HIP(hipEventRecord(D.dep_out, D.stream));
   SV_HIP(hipStreamWaitEvent(user, D.dep_out, 0));
   return SV_OK;
@@ -604,8 +934,9 @@ int sv_timing_enable(int enable) {
 int sv_kernel_time(int device, double* total_ms, uint64_t* launches, uint64_t* signatures) {
   int rc = ensure_init();
   if (rc) return rc;
-  if (device < 0 || device >= (int)g_devs.size()) return fail(SV_ERR_INVALID_ARG, "device index out of range");
-  Device& D = *g_devs[device];
+  Device* Dp = device_arg(device);
+  if (!Dp) return fail(SV_ERR_INVALID_ARG, "device index out of range");
+  Device& D = *Dp;
   std::lock_guard<std::mutex> g(D.mu);
   if (!D.ready) {
     if (total_ms) *total_ms = 0;
@@ -613,7 +944,7 @@ int sv_kernel_time(int device, double* total_ms, uint64_t* launches, uint64_t* s
     if (signatures) *signatures = 0;
     return SV_OK;
   }
-  SV_HIP(hipSetDevice(D.id));
+  SV_HIP(hipSetDevice(D.phys));
   if ((rc = harvest_timing_locked(D))) return rc;
   if (total_ms) *total_ms = D.total_ms;
   if (launches) *launches = D.launches;
@@ -627,7 +958,7 @@ int sv_kernel_time_reset(void) {
   for (Device* D : g_devs) {
     std::lock_guard<std::mutex> g(D->mu);
     if (!D->ready) continue;
-    (void)hipSetDevice(D->id);
+    (void)hipSetDevice(D->phys);
     if ((rc = harvest_timing_locked(*D))) return rc;
     D->total_ms = 0;
     D->launches = 0;
@@ -639,12 +970,35 @@ int sv_kernel_time_reset(void) {
 int sv_device_synchronize(int device) {
   int rc = ensure_init();
   if (rc) return rc;
-  if (device < 0 || device >= (int)g_devs.size()) return fail(SV_ERR_INVALID_ARG, "device index out of range");
-  Device& D = *g_devs[device];
+  Device* Dp = device_arg(device);
+  if (!Dp) return fail(SV_ERR_INVALID_ARG, "device index out of range");
+  Device& D = *Dp;
   std::lock_guard<std::mutex> g(D.mu);
   if (!D.ready) return SV_OK;
-  SV_HIP(hipSetDevice(D.id));
+  SV_HIP(hipSetDevice(D.phys));
   SV_HIP(hipStreamSynchronize(D.stream));
+  return SV_OK;
+}
+
+int sv_workspace_bytes(int device, size_t* bytes) {
+  int rc = ensure_init();
+  if (rc) return rc;
+  Device* Dp = device_arg(device);
+  if (!Dp || !bytes) return fail(SV_ERR_INVALID_ARG, "bad argument");
+  std::lock_guard<std::mutex> g(Dp->mu);
+  *bytes = Dp->ws.cap;
+  return SV_OK;
+}
+
+int sv_pinned_bytes(int device, size_t* bytes) {
+  int rc = ensure_init();
+  if (rc) return rc;
+  Device* Dp = device_arg(device);
+  if (!Dp || !bytes) return fail(SV_ERR_INVALID_ARG, "bad argument");
+  std::lock_guard<std::mutex> g(Dp->mu);
+  size_t b = 0;
+  for (Stage& s : Dp->st) b += s.h_in.cap + s.h_out.cap;
+  *bytes = b;
   return SV_OK;
 }
 

@@ -41,5 +41,12 @@
 #define SV_FENCE() ((void)0)
 #endif
 
+#if defined(__HIPCC__) || defined(__clang__)
 #define SV_UNROLL _Pragma("unroll")
 #define SV_NOUNROLL _Pragma("unroll 1")
+#else
+// g++ (host builds: the CPU path sv_cpu.cpp, tests/native): full unrolling
+// keeps the limb arrays in registers, as on the device
+#define SV_UNROLL _Pragma("GCC unroll 64")
+#define SV_NOUNROLL _Pragma("GCC unroll 1")
+#endif

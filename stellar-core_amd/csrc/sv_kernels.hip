@@ -45,7 +45,16 @@ struct sv_kparams {
   uint64_t* bitmap;       // optional, ceil(n/64) words
   sv_u4* ws;              // workspace: grid threads x SV_SLOT_QUADS (lane-major)
   const sv_u4* btab;      // SV_BTAB_ENTRIES x 9 quads (global copy)
+  uint32_t dbg;           // SV_DBG_* test knobs (sv_set_debug_flags), 0 in production
 };
+// test knobs (include/stellar_sigverify.h sv_set_debug_flags)
+#define SV_DBG_TRIVIAL_PAIR 1u  // every lane takes the fallback pair (h, 1)
+#define SV_DBG_MAX_WINDOWS 2u   // every wave runs 64 windows
+__device__ __forceinline__ int sv_wave_windows(int wl, uint32_t dbg) {
+  int W = (dbg & SV_DBG_MAX_WINDOWS) ? 64 : SV_LAT_MIN_WINDOWS;
+  while (__ballot(wl > W) != 0) ++W;
+  return __builtin_amdgcn_readfirstlane(W);
+}
 
 __device__ __forceinline__ void sv_load_btab_lds(sv_u4* s_btab, const sv_u4* g_btab) {
   for (int i = threadIdx.x; i < SV_BTAB_ENTRIES * (SV_BTAB_STRIDE / 4); i += blockDim.x) s_btab[i] = g_btab[i];
@@ -199,19 +208,16 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_lat_ker
     {
       uint32_t h[8];
       sc_reduce512(h, hram);
-      sc_lattice_reduce(lat, h);
+      sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
     }
     SV_PHASE(2);
     sv_build_ltab(tabA, negA);
     sv_build_ltab(tabR, negR);
     SV_PHASE(3);
 #else
-    bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR);
+    bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
 #endif
-    const int wl = sv_lat_windows(lat.bits);
-    int W = SV_LAT_MIN_WINDOWS;
-    while (__ballot(wl > W) != 0) ++W;
-    W = __builtin_amdgcn_readfirstlane(W);
+    const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
     sv_lat_digits D;
     sv_lat_prepare(D, lat, S, W);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // table stores before the DMA reads
@@ -306,19 +312,16 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   {
     uint32_t h[8];
     sc_reduce512(h, hram);
-    sc_lattice_reduce(lat, h);
+    sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
   }
   SV_PHASE(2);
   sv_build_ltab(tabA, negA);
   sv_build_ltab(tabR, negR);
   SV_PHASE(3);
 #else
-  const bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR);
+  const bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
 #endif
-  const int wl = sv_lat_windows(lat.bits);
-  int W = SV_LAT_MIN_WINDOWS;
-  while (__ballot(wl > W) != 0) ++W;
-  W = __builtin_amdgcn_readfirstlane(W);
+  const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
   const uint32_t flags = (D.rneg ? SV_REC_RNEG : 0u) | (D.top8A ? SV_REC_TOP8A : 0u) |
@@ -458,12 +461,9 @@ __global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
   {
     uint32_t h[8];
     sc_reduce512(h, hram);
-    sc_lattice_reduce(lat, h);
+    sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
   }
-  const int wl = sv_lat_windows(lat.bits);
-  int W = SV_LAT_MIN_WINDOWS;
-  while (__ballot(wl > W) != 0) ++W;
-  W = __builtin_amdgcn_readfirstlane(W);
+  const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
   __syncthreads();  // tables visible to the whole quad
@@ -579,15 +579,39 @@ int sv_debug_phase_cycles(unsigned long long out[8], int reset) {
 #endif
 
 size_t sv_ws_bytes_per_block(void) { return (size_t)SV_BLOCK * SV_SLOT_QUADS * sizeof(sv_u4); }
-// Whole device workspace: the persistent grid's per-lane slots (fused verify
-// kernel, signer) or, split, one chunk's tables + digit records + window counts.
-size_t sv_ws_bytes(unsigned grid) {
+// Signatures one throughput-path launch sequence processes per prep/main
+// chunk: the workspace of a batch of n holds ws_cap(n) = min(n, SV_CHUNK)
+// rounded up to whole workgroups.
+uint64_t sv_ws_cap(uint64_t n) {
+  const uint64_t c = n < SV_CHUNK ? n : SV_CHUNK;
+  return (c + SV_BLOCK - 1) / SV_BLOCK * SV_BLOCK;
+}
+// Device workspace for `grid` persistent workgroups (fused verify kernel,
+// signer: per-lane slots) and, split, a chunk of `cap` signatures (tables +
+// digit records + window counts).  The latency kernel needs none.
+size_t sv_ws_bytes(unsigned grid, uint64_t cap) {
   size_t b = (size_t)grid * sv_ws_bytes_per_block();
 #if SV_LATTICE && SV_SPLIT
-  const size_t s = (size_t)SV_CHUNK * (SV_SLOT_QUADS_L + SV_REC_QUADS) * sizeof(sv_u4) + (SV_CHUNK / 64) * 4;
+  const size_t s = (size_t)cap * (SV_SLOT_QUADS_L + SV_REC_QUADS) * sizeof(sv_u4) + (cap / 64) * 4;
   if (s > b) b = s;
+#else
+  (void)cap;
 #endif
   return b;
+}
+// workspace a verify launch of n signatures on `path` needs
+size_t sv_verify_ws_bytes(int path, unsigned grid, uint64_t n) {
+#if SV_LATTICE
+  if (path == 2) return 0;
+#endif
+#if SV_LATTICE && SV_SPLIT
+  (void)grid;
+  return sv_ws_bytes(0, sv_ws_cap(n));
+#else
+  (void)n;
+  (void)path;
+  return sv_ws_bytes(grid, 0);
+#endif
 }
 #if SV_LATTICE
 #define SV_BTAB_TOTAL (2 * SV_LBTAB_ENTRIES)
@@ -629,9 +653,10 @@ int sv_occupancy_blocks_per_cu(void) {
 #endif
 }
 
+// ws must hold sv_verify_ws_bytes(path, grid, n) bytes.
 hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, const void* sig, const void* msg,
                             const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n,
-                            void* verdict, void* bitmap, void* ws, const void* btab, hipStream_t s) {
+                            void* verdict, void* bitmap, void* ws, const void* btab, uint32_t dbg, hipStream_t s) {
   sv_kparams p;
   p.pk = (const sv_u4*)pk;
   p.sig = (const sv_u4*)sig;
@@ -644,6 +669,7 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
   p.bitmap = (uint64_t*)bitmap;
   p.ws = (sv_u4*)ws;
   p.btab = (const sv_u4*)btab;
+  p.dbg = dbg;
 #if SV_LATTICE
   if (path == 2) {  // SV_PATH_LATENCY
     const unsigned qg = (unsigned)((n + SV_QSIGS - 1) / SV_QSIGS);
@@ -658,13 +684,14 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
 #endif
   (void)path;
 #if SV_LATTICE && SV_SPLIT
-  sv_u4* rec = p.ws + (size_t)SV_CHUNK * SV_SLOT_QUADS_L;
-  uint32_t* wmax = (uint32_t*)(rec + (size_t)SV_CHUNK * SV_REC_QUADS);
-  for (uint64_t start = 0; start < n; start += SV_CHUNK) {
+  const uint64_t cap = sv_ws_cap(n);
+  sv_u4* rec = p.ws + (size_t)cap * SV_SLOT_QUADS_L;
+  uint32_t* wmax = (uint32_t*)(rec + (size_t)cap * SV_REC_QUADS);
+  for (uint64_t start = 0; start < n; start += cap) {
     sv_cparams c;
     c.k = p;
     c.start = start;
-    c.cnt = n - start < SV_CHUNK ? n - start : SV_CHUNK;
+    c.cnt = n - start < cap ? n - start : cap;
     c.rec = rec;
     c.wmax = wmax;
     const unsigned pg = (unsigned)((c.cnt + SV_BLOCK - 1) / SV_BLOCK);

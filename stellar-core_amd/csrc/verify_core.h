@@ -779,7 +779,7 @@ SV_HD bool sv_is_identity(const ge_p3& P) {
 // reduction and the table build.  Returns the pre-verdict and the lane's
 // window count in *W_lane; the caller picks the wave's W >= every W_lane.
 SV_COLD bool sv_lat_pre(sv_lat& lat, const uint32_t A[8], const uint32_t R[8], const uint32_t S[8],
-                        const uint32_t hram[16], sv_u4* tabA, sv_u4* tabR) {
+                        const uint32_t hram[16], sv_u4* tabA, sv_u4* tabR, bool trivial = false) {
   bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
             sv_point_canonical(R);
   ge_p3 negA, negR;
@@ -787,7 +787,7 @@ SV_COLD bool sv_lat_pre(sv_lat& lat, const uint32_t A[8], const uint32_t R[8], c
   ok = ge_frombytes(negR, R, true) && ok;
   uint32_t h[8];
   sc_reduce512(h, hram);
-  sc_lattice_reduce(lat, h);
+  sc_lattice_reduce(lat, h, trivial);
   sv_build_ltab(tabA, negA);
   sv_build_ltab(tabR, negR);
   return ok;
