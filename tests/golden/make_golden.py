@@ -14,7 +14,8 @@ Fixture files (numpy .npz, allow_pickle=False):
                  :643-1629 Zcash), with the reference's expected verdicts.
   valid.npz      deterministic valid set: seed_i = SHA-256("SVSEED"||u64le i),
                  msg_i = SHA-256("SVMSG"||u64le i)  
-  msglen.npz     message lengths 0..300 (multi-block SHA-512 paths)
+  msglen.npz     message lengths 0..512 (1- to 5-block SHA-512 paths, incl. the
+                 128-384 B SCP statement range of config 4)
   adversarial.npz  mutation classes: bit flips in R/S/A/msg,
                  S+L / S+2L / S=L, small-order R and A (+/- bit 255),
                  non-canonical y>=p encodings, off-curve A, mixed-order
@@ -208,7 +209,7 @@ def valid(n=1024):
 
 def msglen():
     rows = Rows()
-    for ln in range(0, 301):
+    for ln in range(0, 513):
         pk, sk = sod_keypair(seed_of(2_000_000 + ln))
         m = hashlib.shake_256(b"LEN" + struct.pack("<Q", ln)).digest(ln) if ln else b""
         s = sod_sign(m, sk)

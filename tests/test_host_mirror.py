@@ -34,6 +34,9 @@ def host(sv):
     lib.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
     lib.svh_set_test_keyed_verifier.argtypes = [ctypes.c_void_p]
     lib.svh_set_keyed_threshold.argtypes = [ctypes.c_size_t]
+    lib.svh_set_cpu_threshold.argtypes = [ctypes.c_size_t]
+    lib.svh_cache_keys.restype = ctypes.c_size_t
+    lib.svh_cache_seed.argtypes = [ctypes.c_uint]
     return lib
 
 
@@ -200,7 +203,7 @@ def test_verify_sig_batch_keyed_path(host, oracle, golden):
         assert _counts(host) == (1, 0)
     finally:
         host.svh_set_test_keyed_verifier(None)
-        host.svh_set_keyed_threshold(4096)
+        host.svh_set_keyed_threshold(256)
         host.svh_cache_clear()
 
 
@@ -384,8 +387,208 @@ def test_gpu_verify_sig_batch_keyed_matches_hashed(host, sv, golden):
             assert rc == 0, host.svh_last_error_string()
             res.append((out.copy(), _counts(host)))
     finally:
-        host.svh_set_keyed_threshold(4096)
+        host.svh_set_keyed_threshold(256)
         host.svh_cache_clear()
     assert (res[0][0] == d["verdict"][rows]).all()
     assert (res[1][0] == res[0][0]).all()
     assert res[0][1] == res[1][1]
+
+
+# ---------------------------------------------------------------- round 2
+class EngineStats(ctypes.Structure):
+    _fields_ = [("gpu_signatures", ctypes.c_uint64), ("gpu_batches", ctypes.c_uint64),
+                ("cpu_signatures", ctypes.c_uint64), ("fallbacks", ctypes.c_uint64)]
+
+
+def _estats(host):
+    s = EngineStats()
+    host.svh_engine_counts_ex(ctypes.byref(s))
+    return s
+
+
+def _batch(host, d, rows):
+    pk = np.ascontiguousarray(d["pk"][rows])
+    sig = np.ascontiguousarray(d["sig"][rows])
+    off = np.ascontiguousarray(d["msg_off"][rows])
+    ln = np.ascontiguousarray(d["msg_len"][rows])
+    msg = np.ascontiguousarray(d["msg"])
+    out = np.full(len(rows), 7, np.uint8)
+    rc = host.svh_verify_sig_batch(pk.ctypes.data_as(ctypes.c_void_p), sig.ctypes.data_as(ctypes.c_void_p), None,
+                                   msg.ctypes.data_as(ctypes.c_void_p), off.ctypes.data_as(ctypes.c_void_p),
+                                   ln.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(len(rows)),
+                                   out.ctypes.data_as(ctypes.c_void_p))
+    return rc, out
+
+
+def test_engine_error_is_never_a_reject(host, golden):
+    """an engine error re-runs the batch on the engine's CPU
+    path -- the mirror returns libsodium's verdicts and raises nothing (the
+    reference's verifySig never throws, SecretKey.cpp:435-468)."""
+    failing = VERIFY_FN(lambda *a: -3)  # SV_ERR_HIP
+    host.svh_set_test_verifier(ctypes.cast(failing, ctypes.c_void_p))
+    host.svh_set_keyed_threshold(0)
+    host.svh_cache_clear()
+    _estats(host)
+    try:
+        for name in ("intree", "msglen", "adversarial"):
+            d = golden[name]
+            rows = np.arange(len(d["verdict"]))
+            rc, out = _batch(host, d, rows)
+            assert rc == 0
+            assert (out == d["verdict"]).all(), name
+        s = _estats(host)
+        assert s.fallbacks == 3 and s.gpu_signatures == 0 and s.cpu_signatures > 0
+    finally:
+        host.svh_set_test_verifier(None)
+        host.svh_set_keyed_threshold(256)
+        host.svh_cache_clear()
+
+
+def test_single_verify_sig_runs_on_cpu_path(host, golden):
+    """verifySig of one signature never pays a GPU round trip: the miss runs on
+    the engine's CPU path (works on this GPU-less host)."""
+    host.svh_set_test_verifier(None)
+    host.svh_cache_clear()
+    host.svh_cache_counts(None, None)
+    _estats(host)
+    d = golden["adversarial"]
+    for i in range(0, len(d["verdict"]), 211):
+        o, ln = int(d["msg_off"][i]), int(d["msg_len"][i])
+        m = d["msg"][o:o + ln].tobytes()
+        assert host.svh_verify_sig(d["pk"][i].tobytes(), d["sig"][i].tobytes(), 64, m, ln) == d["verdict"][i]
+    s = _estats(host)
+    assert s.gpu_signatures == 0 and s.cpu_signatures == len(range(0, len(d["verdict"]), 211))
+    host.svh_cache_clear()
+
+
+class RefCache:
+    """Sequential restatement of RandomEvictionCache<Hash,bool>(0xffff, separatePRNG)
+    (src/util/RandomEvictionCache.h:20-245) with rand_uniform = stellar's pinned
+    libc++ uniform_int_distribution (lib/util/stdrandom.h) over std::minstd_rand."""
+
+    def __init__(self, max_size=0xFFFF, seed=None):
+        self.max, self.gen, self.map, self.ptrs = max_size, 0, {}, []
+        self.x = 1 if seed is None else (seed % 2147483647 or 1)
+
+    def _engine(self):
+        self.x = self.x * 48271 % 2147483647
+        return self.x
+
+    def _uniform(self, lo, hi):
+        r = hi - lo + 1
+        if r == 1:
+            return lo
+        w = (r - 1).bit_length()
+        R, m = 2147483646, 30
+        n = -(-w // m)
+        w0 = w // n
+        y0 = (R >> w0) << w0
+        if R - y0 > y0 // n:
+            n += 1
+            w0 = w // n
+            y0 = (R >> w0) << w0
+        n0 = n - w % n
+        y1 = (R >> (w0 + 1)) << (w0 + 1)
+        while True:
+            s = 0
+            for k in range(n):
+                lim, bits = (y0, w0) if k < n0 else (y1, w0 + 1)
+                while True:
+                    u = self._engine() - 1
+                    if u < lim:
+                        break
+                s = (s << bits) + (u & ((1 << bits) - 1))
+            if s < r:
+                return s + lo
+
+    def get(self, k):
+        self.gen += 1
+        self.map[k][0] = self.gen
+
+    def put(self, k):
+        self.gen += 1
+        if k in self.map:
+            self.map[k][0] = self.gen
+            return
+        self.map[k] = [self.gen]
+        self.ptrs.append(k)
+        if len(self.ptrs) > self.max:
+            a = self._uniform(0, len(self.ptrs) - 1)
+            b = self._uniform(0, len(self.ptrs) - 1)
+            v = a if self.map[self.ptrs[a]][0] < self.map[self.ptrs[b]][0] else b
+            del self.map[self.ptrs[v]]
+            self.ptrs[v], self.ptrs[-1] = self.ptrs[-1], self.ptrs[v]
+            self.ptrs.pop()
+
+
+@pytest.mark.parametrize("keyed", [False, True])
+def test_cache_eviction_matches_sequential_reference(host, hostcore, keyed):
+    """Overfill the 0xffff cache through verifySigBatch (3-phase pending
+    inserts, or the keyed single walk) and compare the surviving keys, their
+    order in the eviction vector, and the hit/miss counts with a sequential
+    restatement of the reference cache fed the same items one by one."""
+    rng = np.random.default_rng(4242)
+    n_distinct = 72000
+    pk = rng.integers(0, 256, (n_distinct, 32), dtype=np.uint8)
+    sig = rng.integers(0, 256, (n_distinct, 64), dtype=np.uint8)
+    msg = rng.integers(0, 256, (n_distinct, 32), dtype=np.uint8)
+    # item stream: every distinct item once plus re-submissions of recent and old ones
+    order = list(range(n_distinct))
+    for k in range(6000):
+        j = int(rng.integers(0, len(order)))
+        order.insert(j + 1, order[max(0, j - int(rng.integers(0, 3000)))])
+    order = np.array(order)
+    if keyed:
+        keys = [sig[i, :32].tobytes() for i in order]  # hc_stub_keyed's "key"
+    else:
+        keys = [hashlib.blake2b(pk[i].tobytes() + sig[i].tobytes() + msg[i].tobytes(), digest_size=32).digest()
+                for i in order]
+    ref = RefCache(seed=1234)
+    hits = misses = 0
+    for k in keys:
+        if k in ref.map:
+            hits += 1
+            ref.get(k)
+        else:
+            misses += 1
+            ref.put(k)
+    stub = ctypes.cast(hostcore.hc_stub_keyed if keyed else hostcore.hc_stub_verify, ctypes.c_void_p)
+    if keyed:
+        host.svh_set_test_keyed_verifier(stub)
+        host.svh_set_keyed_threshold(1)
+    else:
+        host.svh_set_test_verifier(stub)
+        host.svh_set_keyed_threshold(0)
+    host.svh_cache_clear()
+    host.svh_cache_seed(1234)
+    host.svh_cache_counts(None, None)
+    try:
+        P, S = pk[order], sig[order]
+        M = np.ascontiguousarray(msg[order]).reshape(-1)
+        off = np.arange(len(order), dtype=np.uint64) * 32
+        ln = np.full(len(order), 32, np.uint32)
+        out = np.zeros(len(order), np.uint8)
+        pos = 0
+        while pos < len(order):  # batches of varied sizes
+            size = int(rng.choice([1, 7, 1000, 4096, 333]))
+            hi = min(len(order), pos + size)
+            rc = host.svh_verify_sig_batch(P[pos:hi].ctypes.data_as(ctypes.c_void_p),
+                                           np.ascontiguousarray(S[pos:hi]).ctypes.data_as(ctypes.c_void_p), None,
+                                           M.ctypes.data_as(ctypes.c_void_p),
+                                           (off[pos:hi]).ctypes.data_as(ctypes.c_void_p),
+                                           ln[pos:hi].ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(hi - pos),
+                                           out[pos:hi].ctypes.data_as(ctypes.c_void_p))
+            assert rc == 0, host.svh_last_error_string()
+            pos = hi
+        assert out.all()
+        assert _counts(host) == (hits, misses)
+        buf = np.zeros((0x10000, 32), np.uint8)
+        size = host.svh_cache_keys(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(0x10000))
+        assert size == len(ref.ptrs) == 0xFFFF
+        got = [buf[i].tobytes() for i in range(size)]
+        assert got == ref.ptrs
+    finally:
+        host.svh_set_test_verifier(None)
+        host.svh_set_test_keyed_verifier(None)
+        host.svh_set_keyed_threshold(256)
+        host.svh_cache_clear()

@@ -1,0 +1,166 @@
+"""Signature wrapper and transaction-level checks pinned by the reference's own
+tests, fixtures tests/golden/wrapper.json (made by
+tests/golden/make_wrapper.py with libsodium 1.0.18):
+
+  SignatureUtilsTest.cpp:15-32   100 NODE_SEED_i / HASH_ij round trips
+  SignatureUtilsTest.cpp:34-48   HASH_X signers for x = 'A' * 0..64
+  CryptoTests.cpp:272-297        "sign tests"
+  TxEnvelopeTests.cpp:396-736    outer-envelope and multisig outcomes
+
+CPU tests run the C++ mirror with verification on the engine's CPU path (no
+GPU, no test double); the `gpu` variants force every verification through
+the GPU engine (one batch pre-pass, and single calls with the CPU threshold
+at 0)."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import envelopes as ev
+import txset_gen as tg
+from conftest import GOLDEN, REPO
+
+WRAPPER = json.load(open(os.path.join(GOLDEN, "wrapper.json")))
+
+
+@pytest.fixture(scope="module")
+def host(sv):
+    lib = ctypes.CDLL(sv.HOSTLIB_PATH)
+    lib.svh_verify_sig.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                   ctypes.c_size_t]
+    lib.svh_last_error_string.restype = ctypes.c_char_p
+    lib.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+    lib.svh_set_cpu_threshold.argtypes = [ctypes.c_size_t]
+    lib.svh_set_keyed_threshold.argtypes = [ctypes.c_size_t]
+    lib.svh_set_test_verifier(None)
+    return lib
+
+
+class EngineStats(ctypes.Structure):
+    _fields_ = [("gpu_signatures", ctypes.c_uint64), ("gpu_batches", ctypes.c_uint64),
+                ("cpu_signatures", ctypes.c_uint64), ("fallbacks", ctypes.c_uint64)]
+
+
+def engine_stats(host):
+    s = EngineStats()
+    host.svh_engine_counts_ex(ctypes.byref(s))
+    return s
+
+
+def _txset_for(rows_sigs):
+    """[(signers, sigs, hash, needed)] -> ctypes tx set (tests/txset_gen.py layout)."""
+    txs = []
+    for signers, sigs, h, needed in rows_sigs:
+        txs.append({"hash": h, "protocol": 21, "needed": needed, "signers": signers, "sigs": sigs})
+    return tg.to_ctypes(txs)
+
+
+def _run_txset(host, rows_sigs, prefetch):
+    T, S, G = _txset_for(rows_sigs)
+    n = len(rows_sigs)
+    ok = np.zeros(n, np.uint8)
+    used = np.zeros(n, np.uint8)
+    pairs = ctypes.c_uint64()
+    rc = host.svh_check_txset(T, ctypes.c_size_t(n), S, G, prefetch, ok.ctypes.data_as(ctypes.c_void_p),
+                              used.ctypes.data_as(ctypes.c_void_p), ctypes.byref(pairs))
+    assert rc == 0, host.svh_last_error_string()
+    return ok, used
+
+
+def _pubkey_rows():
+    out = []
+    for r in WRAPPER["pubkey_signature"]:
+        signer = {"type": tg.ED25519, "key": bytes.fromhex(r["pk"]), "weight": 1, "payload": b""}
+        sig = {"hint": bytes.fromhex(r["hint"]), "sig": bytes.fromhex(r["sig"])}
+        out.append(([signer], [sig], bytes.fromhex(r["msg"]), 1))
+    return out
+
+
+def _hashx_rows():
+    out = []
+    for r in WRAPPER["hashx"]:
+        signer = {"type": tg.HASH_X, "key": bytes.fromhex(r["key"]), "weight": 1, "payload": b""}
+        sig = {"hint": bytes.fromhex(r["hint"]), "sig": bytes.fromhex(r["sig"])}
+        out.append(([signer], [sig], bytes(32), 1))
+    return out
+
+
+def _sign_test_calls(host):
+    out = []
+    for r in WRAPPER["sign_tests"]:
+        m = bytes.fromhex(r["msg"])
+        out.append(host.svh_verify_sig(bytes.fromhex(r["pk"]), bytes.fromhex(r["sig"]), 64, m, len(m)))
+    return out
+
+
+def _envelope_results(host, case, protocol, prefetch, for_apply=0):
+    es = ev.case_set(case)
+    envs, sigs, ops, signers, accounts = es.arrays()
+    res, _ = ev.check_envelopes(host, envs, sigs, ops, signers, accounts, 1, len(es.accounts), protocol, prefetch,
+                                for_apply)
+    return res[0]
+
+
+def _check_expect(res, want, label):
+    assert int(res["code"]) == want["code"], (label, int(res["code"]), want)
+    for k in ("inner_code", "failed_op", "op_code"):
+        if k in want:
+            assert int(res[k]) == want[k], (label, k, int(res[k]), want)
+
+
+def _all_wrapper_checks(host, prefetch):
+    ok, used = _run_txset(host, _pubkey_rows(), prefetch)
+    assert ok.all() and used.all(), "SignatureUtilsTest.cpp:15-32"
+    ok, used = _run_txset(host, _hashx_rows(), prefetch)
+    assert ok.all() and used.all(), "SignatureUtilsTest.cpp:34-48"
+    assert _sign_test_calls(host) == [r["expect"] for r in WRAPPER["sign_tests"]], "CryptoTests.cpp:272-297"
+    for case in WRAPPER["envelopes"]:
+        for proto, want in case["expect"].items():
+            _check_expect(_envelope_results(host, case, int(proto), prefetch), want, (case["name"], proto, prefetch))
+            if proto == "21":  # the apply path (processSignatures) reaches the same outcome
+                _check_expect(_envelope_results(host, case, 21, prefetch, for_apply=1), want,
+                              (case["name"], "apply", prefetch))
+
+
+def test_wrapper_fixtures_cpu_path(host):
+    """Every reference outcome through the C++ mirror; verifications run on the
+    engine's CPU path (single misses, and the pre-pass batches when no GPU)."""
+    host.svh_cache_clear()
+    host.svh_set_cpu_threshold(1 << 30)
+    try:
+        for prefetch in (0, 1):
+            _all_wrapper_checks(host, prefetch)
+    finally:
+        host.svh_set_cpu_threshold(1)
+    s = engine_stats(host)
+    assert s.gpu_signatures == 0 and s.cpu_signatures > 0
+
+
+def test_envelope_hint_and_size_rules_need_no_verification(host):
+    """'bad signature' (32-byte signature) and 'wrong hint' never reach the
+    verifier (SecretKey.cpp:441-444, SignatureUtils.cpp:129-136)."""
+    engine_stats(host)
+    for name in ("bad signature", "bad signature (wrong hint)"):
+        case = next(c for c in WRAPPER["envelopes"] if c["name"] == name)
+        _check_expect(_envelope_results(host, case, 21, 0), case["expect"]["21"], name)
+    s = engine_stats(host)
+    assert s.gpu_signatures == 0 and s.cpu_signatures == 0
+
+
+@pytest.mark.gpu
+def test_wrapper_fixtures_gpu(host, sv):
+    if sv.device_count() < 1:
+        pytest.skip("no GPU")
+    host.svh_cache_clear()
+    host.svh_set_cpu_threshold(0)  # single verifications go to the GPU too
+    try:
+        engine_stats(host)
+        for prefetch in (0, 1, 2):
+            _all_wrapper_checks(host, prefetch)
+        s = engine_stats(host)
+        assert s.gpu_signatures > 0 and s.cpu_signatures == 0 and s.fallbacks == 0
+    finally:
+        host.svh_set_cpu_threshold(1)
+        host.svh_cache_clear()
