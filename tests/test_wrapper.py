@@ -129,6 +129,7 @@ def test_wrapper_fixtures_cpu_path(host):
     engine's CPU path (single misses, and the pre-pass batches when no GPU)."""
     host.svh_cache_clear()
     host.svh_set_cpu_threshold(1 << 30)
+    engine_stats(host)  # flush earlier tests' counts
     try:
         for prefetch in (0, 1):
             _all_wrapper_checks(host, prefetch)
