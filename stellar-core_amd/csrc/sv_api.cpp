@@ -499,6 +499,10 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
   if (verdict && (rc = ensure_ws(D, sv_verify_ws_bytes(resolve_path(path, chunk), grid_for(D, chunk), chunk))))
     return rc;
   const size_t out_per = (verdict ? 1 : 0) + (keys ? 32 : 0);
+  // one chunk (latency-bound batches): everything on the kernel stream, no
+  // cross-stream event waits
+  const bool single = n <= chunk;
+  hipStream_t up_s = single ? D.stream : D.h2d, down_s = single ? D.stream : D.d2h;
   size_t c = 0;
   for (size_t lo = 0; lo < n; lo += chunk, ++c) {
     Stage& s = D.st[c & 1];
@@ -513,9 +517,11 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     if (verdict && (rc = s.d_verdict.ensure(m))) return rc;
     if (keys && (rc = s.d_keys.ensure(32 * m))) return rc;
     pack(in, lo, m, im, (uint8_t*)s.h_in.p);
-    SV_HIP(hipMemcpyAsync(s.d_in.p, s.h_in.p, im.bytes, hipMemcpyHostToDevice, D.h2d));
-    SV_HIP(hipEventRecord(s.up, D.h2d));
-    SV_HIP(hipStreamWaitEvent(D.stream, s.up, 0));
+    SV_HIP(hipMemcpyAsync(s.d_in.p, s.h_in.p, im.bytes, hipMemcpyHostToDevice, up_s));
+    if (!single) {
+      SV_HIP(hipEventRecord(s.up, D.h2d));
+      SV_HIP(hipStreamWaitEvent(D.stream, s.up, 0));
+    }
     uint8_t* d = (uint8_t*)s.d_in.p;
     const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
     const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
@@ -528,12 +534,14 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
                               s.d_verdict.p, nullptr)))
         return rc;
     }
-    SV_HIP(hipEventRecord(s.done, D.stream));
-    SV_HIP(hipStreamWaitEvent(D.d2h, s.done, 0));
+    if (!single) {
+      SV_HIP(hipEventRecord(s.done, D.stream));
+      SV_HIP(hipStreamWaitEvent(D.d2h, s.done, 0));
+    }
     uint8_t* ho = (uint8_t*)s.h_out.p;
-    if (verdict) SV_HIP(hipMemcpyAsync(ho, s.d_verdict.p, m, hipMemcpyDeviceToHost, D.d2h));
-    if (keys) SV_HIP(hipMemcpyAsync(ho + (verdict ? m : 0), s.d_keys.p, 32 * m, hipMemcpyDeviceToHost, D.d2h));
-    SV_HIP(hipEventRecord(s.down, D.d2h));
+    if (verdict) SV_HIP(hipMemcpyAsync(ho, s.d_verdict.p, m, hipMemcpyDeviceToHost, down_s));
+    if (keys) SV_HIP(hipMemcpyAsync(ho + (verdict ? m : 0), s.d_keys.p, 32 * m, hipMemcpyDeviceToHost, down_s));
+    SV_HIP(hipEventRecord(s.down, down_s));
     s.busy = true;
     s.lo = lo;
     s.m = m;

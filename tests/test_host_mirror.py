@@ -592,3 +592,45 @@ def test_cache_eviction_matches_sequential_reference(host, hostcore, keyed):
         host.svh_set_test_keyed_verifier(None)
         host.svh_set_keyed_threshold(256)
         host.svh_cache_clear()
+
+
+@pytest.mark.gpu
+def test_gpu_config3_full_5000_tx(host, sv, oracle):
+    """BASELINE config 3 at full size: a 5000-tx set with 1-20 ED25519 signers
+    per tx (plus PRE_AUTH_TX / HASH_X / signed-payload signers, colliding-hint
+    wrong keys, unused and short signatures), checked after ONE GPU pre-pass
+    (side table, and seeding the cache); outcomes == the independent Python
+    replay of SignatureChecker.cpp:30-158 with oracle verdicts."""
+    if sv.device_count() < 1:
+        pytest.skip("no GPU")
+    import torch
+    dev = torch.device("cuda", 0)
+
+    def gpu_sign(reqs):
+        seeds = np.frombuffer(b"".join(r[0] for r in reqs), np.uint8).reshape(-1, 32)
+        msgs = np.frombuffer(b"".join(r[1] for r in reqs), np.uint8).reshape(-1, 32)
+        n = len(reqs)
+        ts, tm = torch.from_numpy(seeds.copy()).to(dev), torch.from_numpy(msgs.copy()).to(dev)
+        tpk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        tsig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+        sv.sign_device(0, ts.data_ptr(), tm.data_ptr(), n, tpk.data_ptr(), tsig.data_ptr(),
+                       torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        pk, sg = tpk.cpu().numpy(), tsig.cpu().numpy()
+        return [(pk[i].tobytes(), sg[i].tobytes()) for i in range(n)]
+
+    txs = tg.generate(5000, gpu_sign, seed=2025)
+    tg.add_payload_signatures(txs, _oracle_sign_fn(oracle))
+
+    def verify(pk, sig, msg):
+        return oracle.oracle_ed25519_verify(sig, msg, len(msg), pk) == 0
+
+    want_ok, want_used = tg.replay(txs, verify)
+    host.svh_set_test_verifier(None)
+    for mode in (1, 2):
+        host.svh_cache_clear()
+        ok, used, pairs = _check(host, txs, mode)
+        assert (ok == want_ok).all() and (used == want_used).all(), mode
+        assert pairs > 40000
+    assert 0 < want_ok.sum() < len(txs)
+    host.svh_cache_clear()
