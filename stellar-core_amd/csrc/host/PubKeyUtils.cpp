@@ -113,11 +113,18 @@ inline uint64_t keyBits(Hash const& h) {
 // reference's mValuePtrs); when over capacity, draw two positions of that
 // vector (uniformIndex above, the reference's rand_uniform), evict the less
 // recently accessed entry and swap-remove its position.  get() and put() bump
-// a generation counter exactly as maybeGet()/put() do.  The key -> entry index
-// is a flat linear-probing table (backward-shift deletion) instead of a node
-// map: no allocation per insert/evict.  A slot holds the key's low 32 bits
-// (its home position and a tag that settles almost every mismatch) and the
-// entry id.
+// a generation counter exactly as maybeGet()/put() do.
+//
+// Layout (the batch walk is a long serial chain of these operations, so it is
+// built to miss in cache as rarely as possible):
+//   table_   key -> entry id, flat linear probing with backward-shift deletion;
+//            a slot holds the key's low 32 bits (home position + tag that
+//            settles almost every mismatch) and the entry id + 1;
+//   per insertion-order position: the entry id, its key's low 32 bits and its
+//            last-access generation -- so an eviction (two draws, compare,
+//            unlink) reads only these 1 MB of arrays and the table, never the
+//            32-byte keys;
+//   entries_ key, value, pending owner, back-pointer to the position.
 //
 // Pending entries: a non-keyed verifySigBatch inserts its misses in item
 // order BEFORE verifying them (the value is filled in afterwards), so the
@@ -129,9 +136,9 @@ class RandomEvictionCache {
   static constexpr uint32_t kNone = 0xffffffffu;
   struct Entry {
     Hash key;
-    uint64_t lastAccess;
     uint64_t owner;  // != 0: pending, value not known yet (batch id)
     uint32_t pendIdx;
+    uint32_t pos;    // index in the insertion-order arrays
     bool value;
   };
 
@@ -141,7 +148,9 @@ class RandomEvictionCache {
     table_.assign(cap, 0u);
     mask_ = cap - 1;
     entries_.reserve(maxSize + 1);
-    order_.reserve(maxSize + 1);
+    ordId_.reserve(maxSize + 1);
+    ordTag_.reserve(maxSize + 1);
+    ordGen_.reserve(maxSize + 1);
   }
   void maybeSeed(unsigned seed) { rng_.seed(seed); }
   void prefetch(Hash const& k) const { __builtin_prefetch(&table_[keyBits(k) & mask_]); }
@@ -157,7 +166,7 @@ class RandomEvictionCache {
   // maybeGet() on a found entry
   Entry& touch(uint32_t id) {
     Entry& e = entries_[id];
-    e.lastAccess = ++generation_;
+    ordGen_[e.pos] = ++generation_;
     return e;
   }
   // put(); owner != 0 inserts a pending value
@@ -166,24 +175,29 @@ class RandomEvictionCache {
     const uint32_t id = find(k);
     if (id != kNone) {
       Entry& e = entries_[id];
-      e.lastAccess = generation_;
+      ordGen_[e.pos] = generation_;
       e.value = v;
       e.owner = owner;
       e.pendIdx = pendIdx;
       return;
     }
+    const uint32_t pos = (uint32_t)ordId_.size();
     uint32_t nid;
     if (!freeIds_.empty()) {
       nid = freeIds_.back();
       freeIds_.pop_back();
-      entries_[nid] = Entry{k, generation_, owner, pendIdx, v};
+      entries_[nid] = Entry{k, owner, pendIdx, pos, v};
     } else {
       nid = (uint32_t)entries_.size();
-      entries_.push_back(Entry{k, generation_, owner, pendIdx, v});
+      entries_.push_back(Entry{k, owner, pendIdx, pos, v});
     }
-    insertSlot(k, nid);
-    order_.push_back(nid);
-    if (order_.size() > maxSize_) evictOne();
+    const uint32_t tag = (uint32_t)keyBits(k);
+    insertSlot(tag, nid);
+    ordId_.push_back(nid);
+    ordTag_.push_back(tag);
+    ordGen_.push_back(generation_);
+    if (ordId_.size() > maxSize_) evictOne();
+    if (!freeIds_.empty()) __builtin_prefetch(&entries_[freeIds_.back()], 1);  // the next insert's slot
   }
   // fills in a pending value if the entry is still this batch's
   void resolve(Hash const& k, uint64_t owner, uint32_t pendIdx, bool v) {
@@ -199,28 +213,29 @@ class RandomEvictionCache {
     std::fill(table_.begin(), table_.end(), 0u);
     entries_.clear();
     freeIds_.clear();
-    order_.clear();
+    ordId_.clear();
+    ordTag_.clear();
+    ordGen_.clear();
   }
-  size_t size() const { return order_.size(); }
+  size_t size() const { return ordId_.size(); }
   std::vector<Hash> keysInOrder() const {
     std::vector<Hash> out;
-    out.reserve(order_.size());
-    for (uint32_t id : order_) out.push_back(entries_[id].key);
+    out.reserve(ordId_.size());
+    for (uint32_t id : ordId_) out.push_back(entries_[id].key);
     return out;
   }
 
  private:
-  void insertSlot(Hash const& k, uint32_t id) {
-    const uint64_t tag = keyBits(k) & 0xffffffffu;
+  void insertSlot(uint32_t tag, uint32_t id) {
     size_t s = tag & mask_;
     while (table_[s] != 0) s = (s + 1) & mask_;
-    table_[s] = (tag << 32) | (uint64_t)(id + 1);
+    table_[s] = ((uint64_t)tag << 32) | (uint64_t)(id + 1);
   }
-  void eraseSlot(Hash const& k, uint32_t id) {
-    size_t s = keyBits(k) & mask_;
+  void eraseSlot(uint32_t tag, uint32_t id) {
+    size_t s = tag & mask_;
     while ((uint32_t)table_[s] != id + 1) s = (s + 1) & mask_;
-    // backward-shift deletion keeps every probe chain intact (the home slot
-    // of an occupant is its tag & mask: no entry access needed)
+    // backward-shift deletion keeps every probe chain intact (an occupant's
+    // home slot is its tag & mask)
     size_t hole = s;
     for (size_t j = (hole + 1) & mask_; table_[j] != 0; j = (j + 1) & mask_) {
       const size_t home = (size_t)(table_[j] >> 32) & mask_;
@@ -232,16 +247,25 @@ class RandomEvictionCache {
     table_[hole] = 0;
   }
   void evictOne() {
-    const size_t sz = order_.size();
+    const size_t sz = ordId_.size();
     if (sz == 0) return;
     const size_t ia = uniformIndex(rng_, 0, sz - 1);
     const size_t ib = uniformIndex(rng_, 0, sz - 1);
-    const size_t iv = entries_[order_[ia]].lastAccess < entries_[order_[ib]].lastAccess ? ia : ib;
-    const uint32_t victim = order_[iv];
-    eraseSlot(entries_[victim].key, victim);
+    const size_t iv = ordGen_[ia] < ordGen_[ib] ? ia : ib;
+    const uint32_t victim = ordId_[iv];
+    eraseSlot(ordTag_[iv], victim);
     freeIds_.push_back(victim);
-    std::swap(order_[iv], order_.back());
-    order_.pop_back();
+    // swap-remove position iv (the reference's swap with mValuePtrs.back())
+    const size_t last = sz - 1;
+    if (iv != last) {
+      ordId_[iv] = ordId_[last];
+      ordTag_[iv] = ordTag_[last];
+      ordGen_[iv] = ordGen_[last];
+      entries_[ordId_[iv]].pos = (uint32_t)iv;
+    }
+    ordId_.pop_back();
+    ordTag_.pop_back();
+    ordGen_.pop_back();
   }
   size_t maxSize_;
   size_t mask_;
@@ -249,7 +273,8 @@ class RandomEvictionCache {
   std::vector<uint64_t> table_;
   std::vector<Entry> entries_;
   std::vector<uint32_t> freeIds_;
-  std::vector<uint32_t> order_;
+  std::vector<uint32_t> ordId_, ordTag_;
+  std::vector<uint64_t> ordGen_;
   std::minstd_rand rng_;  // stellar_default_random_engine, src/util/Math.h:26
 };
 
@@ -266,32 +291,45 @@ std::atomic<size_t> gCpuThreshold{1};
 
 using Item = PubKeyUtils::VerifyItem;
 
-// SoA copy of items[rows] for the test hooks (the engine itself gathers).
-struct Packed {
-  std::vector<uint8_t> pk, sig, msg;
-  std::vector<uint64_t> off;
+// Per-thread scratch reused across calls: a large batch does not pay fresh
+// page faults for its index, key and pointer arrays every time.
+struct Scratch {
+  std::vector<size_t> rows, missRows, missItems;
+  std::vector<Hash> keys;
+  std::vector<uint8_t> verdict, mv;
+  std::vector<uint32_t> ref;
+  std::vector<const uint8_t*> pk, sig, msg;
   std::vector<uint32_t> len;
-  Packed(std::vector<Item> const& items, std::vector<size_t> const& rows) {
-    const size_t n = rows.size();
-    pk.resize(32 * n);
-    sig.resize(64 * n);
-    off.resize(n);
-    len.resize(n);
-    size_t total = 0;
-    for (size_t r : rows) total += items[r].msg.size();
-    msg.resize(std::max<size_t>(1, total));
-    size_t pos = 0;
-    for (size_t i = 0; i < n; ++i) {
-      Item const& it = items[rows[i]];
-      std::memcpy(&pk[32 * i], it.key->ed25519().data(), 32);
-      std::memcpy(&sig[64 * i], it.signature->data(), 64);
-      off[i] = pos;
-      len[i] = (uint32_t)it.msg.size();
-      if (len[i]) std::memcpy(&msg[pos], it.msg.data(), len[i]);
-      pos += len[i];
-    }
-  }
+  // SoA copy for the test hooks (the engine itself gathers)
+  std::vector<uint8_t> ppk, psig, pmsg;
+  std::vector<uint64_t> poff;
+  std::vector<uint32_t> plen;
 };
+Scratch& scratch() {
+  static thread_local Scratch s;
+  return s;
+}
+
+void packForTestHook(std::vector<Item> const& items, std::vector<size_t> const& rows, Scratch& st) {
+  const size_t n = rows.size();
+  st.ppk.resize(32 * n);
+  st.psig.resize(64 * n);
+  st.poff.resize(n);
+  st.plen.resize(n);
+  size_t total = 0;
+  for (size_t r : rows) total += items[r].msg.size();
+  st.pmsg.resize(std::max<size_t>(1, total));
+  size_t pos = 0;
+  for (size_t i = 0; i < n; ++i) {
+    Item const& it = items[rows[i]];
+    std::memcpy(&st.ppk[32 * i], it.key->ed25519().data(), 32);
+    std::memcpy(&st.psig[64 * i], it.signature->data(), 64);
+    st.poff[i] = pos;
+    st.plen[i] = (uint32_t)it.msg.size();
+    if (st.plen[i]) std::memcpy(&st.pmsg[pos], it.msg.data(), st.plen[i]);
+    pos += st.plen[i];
+  }
+}
 
 // CPU path over items[rows] (the engine's own algorithm, host build).
 void cpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, uint8_t* verdict) {
@@ -319,25 +357,29 @@ int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, u
   const size_t n = rows.size();
   static_assert(sizeof(Hash) == 32, "Hash must be 32 contiguous bytes");
   uint8_t* kb = reinterpret_cast<uint8_t*>(keys);
+  Scratch& st = scratch();
   if (keys) {
     if (PubKeyUtils::KeyedBatchVerifyFn tk = gTestKeyedVerifier.load()) {
-      Packed p(items, rows);
-      return tk(p.pk.data(), p.sig.data(), p.msg.data(), p.off.data(), p.len.data(), n, verdict, kb);
+      packForTestHook(items, rows, st);
+      return tk(st.ppk.data(), st.psig.data(), st.pmsg.data(), st.poff.data(), st.plen.data(), n, verdict, kb);
     }
   } else if (PubKeyUtils::BatchVerifyFn tv = gTestVerifier.load()) {
-    Packed p(items, rows);
-    return tv(p.pk.data(), p.sig.data(), p.msg.data(), p.off.data(), p.len.data(), n, verdict);
+    packForTestHook(items, rows, st);
+    return tv(st.ppk.data(), st.psig.data(), st.pmsg.data(), st.poff.data(), st.plen.data(), n, verdict);
   }
-  std::vector<const uint8_t*> pk(n), sig(n), msg(n);
-  std::vector<uint32_t> len(n);
+  st.pk.resize(n);
+  st.sig.resize(n);
+  st.msg.resize(n);
+  st.len.resize(n);
   for (size_t i = 0; i < n; ++i) {
     Item const& it = items[rows[i]];
-    pk[i] = it.key->ed25519().data();
-    sig[i] = it.signature->data();
-    msg[i] = it.msg.data();
-    len[i] = (uint32_t)it.msg.size();
+    st.pk[i] = it.key->ed25519().data();
+    st.sig[i] = it.signature->data();
+    st.msg[i] = it.msg.data();
+    st.len[i] = (uint32_t)it.msg.size();
   }
-  return sv_ed25519_verify_batch_gather(pk.data(), sig.data(), msg.data(), len.data(), n, verdict, kb, nullptr);
+  return sv_ed25519_verify_batch_gather(st.pk.data(), st.sig.data(), st.msg.data(), st.len.data(), n, verdict, kb,
+                                        nullptr);
 }
 
 }  // namespace
@@ -355,8 +397,9 @@ Hash verifySigCacheKey(PublicKey const& key, Signature const& signature, ByteSli
 std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vector<Hash>* keysOut) {
   const size_t n = items.size();
   std::vector<bool> out(n, false);
-  std::vector<size_t> rows;  // eligible items
-  rows.reserve(n);
+  Scratch& sc = scratch();
+  std::vector<size_t>& rows = sc.rows;  // eligible items
+  rows.clear();
   for (size_t i = 0; i < n; ++i) {
     if (items[i].key->type() != PUBLIC_KEY_TYPE_ED25519)
       throw std::invalid_argument("verifySigBatch: non-ed25519 key");  // releaseAssert, SecretKey.cpp:440
@@ -366,8 +409,10 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
   if (keysOut) keysOut->assign(n, Hash{});
   const size_t E = rows.size();
   if (E == 0) return out;
-  std::vector<Hash> keys(E);
-  std::vector<uint8_t> verdict(E, 0);
+  std::vector<Hash>& keys = sc.keys;
+  keys.resize(E);
+  std::vector<uint8_t>& verdict = sc.verdict;
+  verdict.assign(E, 0);
 
   const size_t thr = gKeyedThreshold.load();
   if (thr != 0 && E >= thr && gTestVerifier.load() == nullptr) {
@@ -396,8 +441,10 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
   } else {
     hostKeys(items, rows, keys.data());
     // phase 1: walk the cache in item order; misses are inserted pending
-    std::vector<size_t> missRows;  // item of each distinct miss
-    std::vector<uint32_t> ref(E, RandomEvictionCache::kNone);
+    std::vector<size_t>& missRows = sc.missRows;  // eligible index of each distinct miss
+    missRows.clear();
+    std::vector<uint32_t>& ref = sc.ref;
+    ref.assign(E, RandomEvictionCache::kNone);
     uint64_t owner;
     {
       std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
@@ -426,9 +473,11 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     }
     // phase 2: verify the misses (outside the lock: the engine call is long)
     const size_t M = missRows.size();
-    std::vector<size_t> missItems(M);
+    std::vector<size_t>& missItems = sc.missItems;
+    missItems.resize(M);
     for (size_t m = 0; m < M; ++m) missItems[m] = rows[missRows[m]];
-    std::vector<uint8_t> mv(M, 0);
+    std::vector<uint8_t>& mv = sc.mv;
+    mv.assign(M, 0);
     if (M > 0) {
       if (M <= gCpuThreshold.load() && gTestVerifier.load() == nullptr) {
         cpuVerify(items, missItems, mv.data());
