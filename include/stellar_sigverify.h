@@ -119,6 +119,18 @@ int sv_ed25519_verify_batch_gather(const uint8_t* const* pk, const uint8_t* cons
                                    const sv_opts* opts);
 
 /*
+ * Same, with a callback for overlapping the caller's work with the GPU:
+ * keys_ready(ctx) is called exactly once on success, on the calling thread,
+ * as soon as every key is in `keys` -- for a batch that fits one staging chunk
+ * on one slot, while the verify kernels are still running -- and the call
+ * returns once the verdicts are in `verdict`.  keys_ready must not call into
+ * this library.  On an error return keys_ready may or may not have run.
+ */
+int sv_ed25519_verify_batch_gather_cb(const uint8_t* const* pk, const uint8_t* const* sig,
+                                      const uint8_t* const* msg, const uint32_t* msg_len, size_t n, uint8_t* verdict,
+                                      uint8_t* keys, void (*keys_ready)(void* ctx), void* ctx, const sv_opts* opts);
+
+/*
  * CPU path: the engine's own per-signature algorithm (csrc/verify_core.h,
  * the half-size equation of csrc/lattice.h) compiled for the host, on
  * `threads` threads (0: the machine's hardware concurrency, capped at 16).

@@ -62,7 +62,7 @@ EXPORTED_SYMBOLS = (
     "sv_ed25519_sign_device", "sv_timing_enable", "sv_kernel_time", "sv_kernel_time_reset",
     "sv_device_synchronize", "sv_verify_cache_keys", "sv_ed25519_verify_batch_keyed", "sv_sha256_batch",
     "sv_verify_cache_keys_device", "sv_sha256_device", "sv_set_kernel_path",
-    "sv_ed25519_verify_batch_gather", "sv_ed25519_verify_batch_cpu", "sv_ed25519_verify_cpu",
+    "sv_ed25519_verify_batch_gather", "sv_ed25519_verify_batch_gather_cb", "sv_ed25519_verify_batch_cpu", "sv_ed25519_verify_cpu",
     "sv_set_device_map", "sv_set_min_shard", "sv_set_debug_flags", "sv_workspace_bytes", "sv_pinned_bytes",
 )
 

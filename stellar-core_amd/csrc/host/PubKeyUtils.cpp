@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <mutex>
 #include <random>
@@ -323,7 +324,7 @@ void packForTestHook(std::vector<Item> const& items, std::vector<size_t> const& 
   for (size_t i = 0; i < n; ++i) {
     Item const& it = items[rows[i]];
     std::memcpy(&st.ppk[32 * i], it.key->ed25519().data(), 32);
-    std::memcpy(&st.psig[64 * i], it.signature->data(), 64);
+    std::memcpy(&st.psig[64 * i], it.signature.data(), 64);
     st.poff[i] = pos;
     st.plen[i] = (uint32_t)it.msg.size();
     if (st.plen[i]) std::memcpy(&st.pmsg[pos], it.msg.data(), st.plen[i]);
@@ -335,7 +336,7 @@ void packForTestHook(std::vector<Item> const& items, std::vector<size_t> const& 
 void cpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, uint8_t* verdict) {
   parallelFor(rows.size(), 4, [&](size_t i) {
     Item const& it = items[rows[i]];
-    verdict[i] = sv_ed25519_verify_cpu(it.key->ed25519().data(), it.signature->data(), it.msg.data(),
+    verdict[i] = sv_ed25519_verify_cpu(it.key->ed25519().data(), it.signature.data(), it.msg.data(),
                                        it.msg.size()) == 1
                      ? 1
                      : 0;
@@ -346,14 +347,19 @@ void cpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, 
 void hostKeys(std::vector<Item> const& items, std::vector<size_t> const& rows, Hash* keys) {
   parallelFor(rows.size(), 256, [&](size_t i) {
     Item const& it = items[rows[i]];
-    keys[i] = PubKeyUtils::verifySigCacheKey(*it.key, *it.signature, it.msg);
+    keys[i] = PubKeyUtils::verifySigCacheKey(*it.key, it.signature, it.msg);
   });
 }
 
 // GPU engine over items[rows] (gather: the engine packs straight from the
 // items); keys != nullptr also returns the cache keys.  Returns the engine's
 // status; the caller falls back to the CPU path on any error.
-int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, uint8_t* verdict, Hash* keys) {
+void runCallback(void* ctx) { (*static_cast<std::function<void()>*>(ctx))(); }
+
+// keysReady (keyed passes): run once the keys are in `keys`; the engine calls
+// it while the GPU still verifies (one-chunk batches), else it runs here.
+int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, uint8_t* verdict, Hash* keys,
+              std::function<void()>* keysReady = nullptr) {
   const size_t n = rows.size();
   static_assert(sizeof(Hash) == 32, "Hash must be 32 contiguous bytes");
   uint8_t* kb = reinterpret_cast<uint8_t*>(keys);
@@ -361,7 +367,9 @@ int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, u
   if (keys) {
     if (PubKeyUtils::KeyedBatchVerifyFn tk = gTestKeyedVerifier.load()) {
       packForTestHook(items, rows, st);
-      return tk(st.ppk.data(), st.psig.data(), st.pmsg.data(), st.poff.data(), st.plen.data(), n, verdict, kb);
+      const int rc = tk(st.ppk.data(), st.psig.data(), st.pmsg.data(), st.poff.data(), st.plen.data(), n, verdict, kb);
+      if (rc == SV_OK && keysReady) (*keysReady)();
+      return rc;
     }
   } else if (PubKeyUtils::BatchVerifyFn tv = gTestVerifier.load()) {
     packForTestHook(items, rows, st);
@@ -374,10 +382,13 @@ int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, u
   for (size_t i = 0; i < n; ++i) {
     Item const& it = items[rows[i]];
     st.pk[i] = it.key->ed25519().data();
-    st.sig[i] = it.signature->data();
+    st.sig[i] = it.signature.data();
     st.msg[i] = it.msg.data();
     st.len[i] = (uint32_t)it.msg.size();
   }
+  if (keysReady)
+    return sv_ed25519_verify_batch_gather_cb(st.pk.data(), st.sig.data(), st.msg.data(), st.len.data(), n, verdict,
+                                             kb, runCallback, keysReady, nullptr);
   return sv_ed25519_verify_batch_gather(st.pk.data(), st.sig.data(), st.msg.data(), st.len.data(), n, verdict, kb,
                                         nullptr);
 }
@@ -387,6 +398,10 @@ int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, u
 namespace PubKeyUtils {
 
 Hash verifySigCacheKey(PublicKey const& key, Signature const& signature, ByteSlice const& bin) {
+  return verifySigCacheKey(key, ByteSlice(signature), bin);
+}
+
+Hash verifySigCacheKey(PublicKey const& key, ByteSlice const& signature, ByteSlice const& bin) {
   hostcrypto::Blake2b256 h;
   h.add(key.ed25519().data(), 32);
   h.add(signature.data(), signature.size());
@@ -403,7 +418,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
   for (size_t i = 0; i < n; ++i) {
     if (items[i].key->type() != PUBLIC_KEY_TYPE_ED25519)
       throw std::invalid_argument("verifySigBatch: non-ed25519 key");  // releaseAssert, SecretKey.cpp:440
-    if (items[i].signature->size() != 64) continue;                   // SecretKey.cpp:441-444
+    if (items[i].signature.size() != 64) continue;                   // SecretKey.cpp:441-444
     rows.push_back(i);
   }
   if (keysOut) keysOut->assign(n, Hash{});
@@ -416,28 +431,56 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
 
   const size_t thr = gKeyedThreshold.load();
   if (thr != 0 && E >= thr && gTestVerifier.load() == nullptr) {
-    // keyed: every eligible item verified and hashed in one engine pass
-    if (gpuVerify(items, rows, verdict.data(), keys.data()) == SV_OK) {
+    // keyed: every eligible item verified and hashed in one engine pass.  The
+    // cache walk (phase 1: hits, misses inserted pending in item order) runs
+    // as soon as the keys are back, overlapping the GPU's verification; the
+    // pending values are filled in once the verdicts arrive (phase 3).
+    std::vector<uint8_t>& hit = sc.mv;
+    hit.assign(E, 0);
+    uint64_t owner = 0;
+    bool walked = false;
+    std::function<void()> phase1 = [&] {
+      std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
+      owner = ++gBatchId;
+      for (size_t e = 0; e < E; ++e) {
+        if (e + 8 < E) gVerifySigCache.prefetch(keys[e + 8]);
+        const uint32_t id = gVerifySigCache.find(keys[e]);
+        if (id != RandomEvictionCache::kNone) {
+          auto const& ent = gVerifySigCache.at(id);
+          if (ent.owner == 0 || ent.owner == owner) {  // cached, or an earlier item of this batch
+            ++gVerifyCacheHit;
+            auto& t = gVerifySigCache.touch(id);
+            if (t.owner == 0) {
+              hit[e] = 1;
+              out[rows[e]] = t.value;
+            }
+            continue;
+          }
+        }
+        ++gVerifyCacheMiss;
+        gVerifySigCache.put(keys[e], false, owner, (uint32_t)e);
+      }
+      walked = true;
+    };
+    if (gpuVerify(items, rows, verdict.data(), keys.data(), &phase1) == SV_OK) {
       gGpuSigs += E;
       gGpuBatches += 1;
     } else {
       ++gFallbacks;
-      hostKeys(items, rows, keys.data());
+      if (!walked) {
+        hostKeys(items, rows, keys.data());
+        phase1();
+      }
       cpuVerify(items, rows, verdict.data());
     }
-    std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
-    for (size_t e = 0; e < E; ++e) {
-      if (e + 8 < E) gVerifySigCache.prefetch(keys[e + 8]);
-      const uint32_t id = gVerifySigCache.find(keys[e]);
-      if (id != RandomEvictionCache::kNone && gVerifySigCache.at(id).owner == 0) {
-        ++gVerifyCacheHit;
-        out[rows[e]] = gVerifySigCache.touch(id).value;
-      } else {
-        ++gVerifyCacheMiss;
-        gVerifySigCache.put(keys[e], verdict[e] != 0);
-        out[rows[e]] = verdict[e] != 0;
-      }
+    if (!walked) phase1();  // (not reached: the engine ran it on success)
+    {
+      std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
+      for (size_t e = 0; e < E; ++e)
+        if (!hit[e]) gVerifySigCache.resolve(keys[e], owner, (uint32_t)e, verdict[e] != 0);
     }
+    for (size_t e = 0; e < E; ++e)
+      if (!hit[e]) out[rows[e]] = verdict[e] != 0;
   } else {
     hostKeys(items, rows, keys.data());
     // phase 1: walk the cache in item order; misses are inserted pending
@@ -526,7 +569,7 @@ void verifyBatchUncached(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
 }
 
 bool verifySig(PublicKey const& key, Signature const& signature, ByteSlice const& bin) {
-  std::vector<VerifyItem> one{VerifyItem{&key, &signature, bin}};
+  std::vector<VerifyItem> one{VerifyItem{&key, ByteSlice(signature), bin}};
   return verifySigBatch(one, nullptr)[0];
 }
 

@@ -71,9 +71,11 @@ struct ByteSlice {
 
 namespace PubKeyUtils {
 
+// One verification: borrowed key, signature bytes (size != 64 is rejected
+// before any cache interaction, as in verifySig) and message.
 struct VerifyItem {
   PublicKey const* key;
-  Signature const* signature;
+  ByteSlice signature;
   ByteSlice msg;
 };
 
@@ -98,6 +100,7 @@ void flushVerifySigCacheCounts(uint64_t& hits, uint64_t& misses);
 
 // BLAKE2b-256(pk || sig || msg), SecretKey.cpp:50-61
 Hash verifySigCacheKey(PublicKey const& key, Signature const& signature, ByteSlice const& bin);
+Hash verifySigCacheKey(PublicKey const& key, ByteSlice const& signature, ByteSlice const& bin);
 
 // Engine override for tests (cf. the reference's BUILD_TESTS hooks such as
 // AlwaysValidSignatureChecker, SignatureChecker.h:41-63): when set, GPU-bound

@@ -111,12 +111,11 @@ void SignatureBatchPrefetch::run(bool seedCache) {
   const uint8_t* msg = msg_.empty() ? nullptr : msg_.data();
   if (seedCache) {
     std::vector<PublicKey> keys(n);
-    std::vector<Signature> sigs(n);
     std::vector<PubKeyUtils::VerifyItem> items(n);
     for (size_t i = 0; i < n; ++i) {
       std::memcpy(keys[i].ed25519().data(), &pk_[32 * i], 32);
-      sigs[i].assign(&sig_[64 * i], &sig_[64 * i] + 64);
-      items[i] = PubKeyUtils::VerifyItem{&keys[i], &sigs[i], ByteSlice(msg ? msg + off_[i] : nullptr, len_[i])};
+      items[i] = PubKeyUtils::VerifyItem{&keys[i], ByteSlice(&sig_[64 * i], 64),
+                                         ByteSlice(msg ? msg + off_[i] : nullptr, len_[i])};
     }
     std::vector<bool> v = PubKeyUtils::verifySigBatch(items);
     for (size_t i = 0; i < n; ++i) verdict_[i] = v[i] ? 1 : 0;

@@ -14,6 +14,11 @@
 // overlaps another's engine call.  The engine and the verify cache are
 // thread-safe, so verdicts do not depend on the worker count.
 //
+// Queue layout: fixed records (key, signature bytes) plus one byte arena for
+// the messages; a flushing worker swaps the whole queue out under the lock, so
+// enqueueing costs one short critical section and no allocation per item
+// (submit() allocates its promise).
+//
 // Engine errors never reach producers: verifySigBatch re-runs a failed batch
 // on the CPU path (PubKeyUtils.h).
 #pragma once
@@ -21,9 +26,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
-#include <deque>
 #include <future>
-#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -43,9 +46,9 @@ class VerifyMicroBatcher {
   VerifyMicroBatcher& operator=(VerifyMicroBatcher const&) = delete;
 
   // Thread-safe.  The future carries the verdict.
-  std::future<bool> submit(PublicKey const& key, Signature const& sig, ByteSlice const& msg);
+  std::future<bool> submit(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg);
   // Thread-safe, fire and forget: the verdict lands in the verify cache only.
-  void post(PublicKey const& key, Signature const& sig, ByteSlice const& msg);
+  void post(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg);
   // Blocks until every item enqueued before the call has been verified.
   void drain();
 
@@ -63,14 +66,21 @@ class VerifyMicroBatcher {
   std::vector<double> latencies() const;
 
  private:
-  struct Item {
+  using Clock = std::chrono::steady_clock;
+  struct Rec {
     PublicKey key;
-    Signature sig;
-    std::vector<uint8_t> msg;
-    std::unique_ptr<std::promise<bool>> done;  // submit() only
-    std::chrono::steady_clock::time_point t0;
+    uint8_t sig[64];
+    uint32_t sigLen;
+    uint32_t msgLen;
+    uint64_t msgOff;                // into the arena
+    std::promise<bool>* done;       // submit() only
+    Clock::time_point t0;           // recordLatency only
   };
-  void enqueue(Item&& it);
+  struct Queue {
+    std::vector<Rec> recs;
+    std::vector<uint8_t> arena;
+  };
+  void enqueue(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg, std::promise<bool>* done);
   void run();
 
   const size_t mMaxBatch;
@@ -79,7 +89,8 @@ class VerifyMicroBatcher {
   mutable std::mutex mMu;
   std::condition_variable mCv;
   std::condition_variable mDoneCv;
-  std::deque<Item> mQueue;
+  Queue mQ;
+  Clock::time_point mOldest;  // arrival of the oldest queued item
   bool mStop = false;
   uint64_t mEnqueued = 0, mCompleted = 0;
   Stats mStats;

@@ -88,14 +88,12 @@ int svh_verify_sig_batch(const uint8_t* pk, const uint8_t* sig, const uint32_t* 
                          const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* verdict) {
   try {
     std::vector<PublicKey> keys(n);
-    std::vector<Signature> sigs(n);
     std::vector<PubKeyUtils::VerifyItem> items(n);
     for (size_t i = 0; i < n; ++i) {
       std::memcpy(keys[i].ed25519().data(), pk + 32 * i, 32);
       const uint32_t sl = sig_len ? sig_len[i] : 64;
       if (sl > 64) throw std::invalid_argument("signature longer than 64 bytes");
-      sigs[i].assign(sig + 64 * i, sig + 64 * i + sl);
-      items[i] = PubKeyUtils::VerifyItem{&keys[i], &sigs[i], ByteSlice(msg + msg_off[i], msg_len[i])};
+      items[i] = PubKeyUtils::VerifyItem{&keys[i], ByteSlice(sig + 64 * i, sl), ByteSlice(msg + msg_off[i], msg_len[i])};
     }
     auto v = PubKeyUtils::verifySigBatch(items);
     for (size_t i = 0; i < n; ++i) verdict[i] = v[i] ? 1 : 0;
@@ -255,10 +253,9 @@ int svh_mb_run_ex(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, con
       th.emplace_back([&, p] {
         std::vector<std::pair<size_t, std::future<bool>>> futs;
         PublicKey k;
-        Signature s(64);
         for (size_t i = (size_t)p; i < n; i += (size_t)producers) {
           std::memcpy(k.ed25519().data(), pk + 32 * i, 32);
-          std::memcpy(s.data(), sig + 64 * i, 64);
+          const ByteSlice s(sig + 64 * i, 64);
           const ByteSlice m(msg + msg_off[i], msg_len[i]);
           if (fire_and_forget) mb.post(k, s, m);
           else futs.emplace_back(i, mb.submit(k, s, m));

@@ -231,7 +231,7 @@ SV_COLD void sc_lattice_reduce(sv_lat& o, const uint32_t h[8], bool trivial = fa
   tb[0] = 1;
   bool bneg = false;  // sign of t for b; t for a has the opposite sign
   bool bail = trivial;
-  SV_NOUNROLL for (int it = 0; it < (trivial ? 0 : SV_LAT_MAX_ITERS); ++it) {
+  SV_NOUNROLL for (int it = 0; it < SV_LAT_MAX_ITERS && !trivial; ++it) {
     uint32_t hi = 0;
     SV_UNROLL for (int i = SV_LAT_SPLIT_WORDS; i < 8; ++i) hi |= b[i];
     if (hi == 0) break;

@@ -148,7 +148,7 @@ struct HostBuf {
 struct Stage {
   HostBuf h_in, h_out;
   DevBuf d_in, d_verdict, d_keys;
-  hipEvent_t up = nullptr, done = nullptr, down = nullptr;
+  hipEvent_t up = nullptr, done = nullptr, down = nullptr, keys_down = nullptr;
   bool busy = false;  // a chunk's D2H is pending on `down`
   size_t lo = 0, m = 0;
 };
@@ -224,6 +224,7 @@ int init_device(Device& D) {
     SV_HIP(hipEventCreateWithFlags(&s.up, hipEventDisableTiming));
     SV_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
     SV_HIP(hipEventCreateWithFlags(&s.down, hipEventDisableTiming));
+    SV_HIP(hipEventCreateWithFlags(&s.keys_down, hipEventDisableTiming));
   }
   SV_HIP(hipMalloc(&D.btab, sv_btab_bytes()));
   SV_HIP(sv_launch_btab_init((uint32_t*)D.btab, D.stream));
@@ -250,7 +251,8 @@ void release_device(Device& D) {
     if (s.up) (void)hipEventDestroy(s.up);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.down) (void)hipEventDestroy(s.down);
-    s.up = s.done = s.down = nullptr;
+    if (s.keys_down) (void)hipEventDestroy(s.keys_down);
+    s.up = s.done = s.down = s.keys_down = nullptr;
   }
   D.msg.release(); D.off.release(); D.len.release(); D.keys.release(); D.h_sha.release();
   D.ws.release();
@@ -489,10 +491,16 @@ int drain_stage(Stage& s, uint8_t* verdict, uint8_t* keys) {
   return SV_OK;
 }
 
+typedef void (*KeysReadyFn)(void*);
+
 // Host-buffer slice on one slot, pipelined over staging chunks: verdicts
 // (verdict != null) and/or BLAKE2b cache keys (keys != null) into the
-// caller's arrays.
-int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, int path) {
+// caller's arrays.  keys_cb (optional, with keys and verdict): called once
+// every key is in `keys` -- for a one-chunk batch while the verify kernels
+// are still running, so the caller's cache walk overlaps them; *cb_done
+// records that it ran.
+int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, int path,
+                      KeysReadyFn keys_cb, void* cb_ctx, bool* cb_done) {
   const size_t chunk = std::min(n, stage_chunk());
   int rc;
   // the largest launch first, so the workspace never grows under a running kernel
@@ -528,6 +536,14 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     if (keys)
       SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m, s.d_keys.p,
                             D.stream));
+    const bool early = single && keys_cb && keys && verdict;
+    if (early) {
+      // keys down on the D2H stream while the verify kernels run
+      SV_HIP(hipEventRecord(s.done, D.stream));
+      SV_HIP(hipStreamWaitEvent(D.d2h, s.done, 0));
+      SV_HIP(hipMemcpyAsync((uint8_t*)s.h_out.p + m, s.d_keys.p, 32 * m, hipMemcpyDeviceToHost, D.d2h));
+      SV_HIP(hipEventRecord(s.keys_down, D.d2h));
+    }
     if (verdict) {
       const int mode = im.var ? 1 : (in.fixed == 32 ? 0 : 2);
       if ((rc = launch_locked(D, mode, path, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m,
@@ -540,23 +556,31 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     }
     uint8_t* ho = (uint8_t*)s.h_out.p;
     if (verdict) SV_HIP(hipMemcpyAsync(ho, s.d_verdict.p, m, hipMemcpyDeviceToHost, down_s));
-    if (keys) SV_HIP(hipMemcpyAsync(ho + (verdict ? m : 0), s.d_keys.p, 32 * m, hipMemcpyDeviceToHost, down_s));
+    if (keys && !early)
+      SV_HIP(hipMemcpyAsync(ho + (verdict ? m : 0), s.d_keys.p, 32 * m, hipMemcpyDeviceToHost, down_s));
     SV_HIP(hipEventRecord(s.down, down_s));
     s.busy = true;
     s.lo = lo;
     s.m = m;
+    if (early) {
+      SV_HIP(hipEventSynchronize(s.keys_down));
+      std::memcpy(keys + 32 * lo, ho + m, 32 * m);
+      keys_cb(cb_ctx);
+      *cb_done = true;
+    }
   }
   for (Stage& s : D.st)
     if ((rc = drain_stage(s, verdict, keys))) return rc;
   return SV_OK;
 }
 
-int host_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, int path) {
+int host_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, int path,
+               KeysReadyFn keys_cb = nullptr, void* cb_ctx = nullptr, bool* cb_done = nullptr) {
   std::lock_guard<std::mutex> g(D.mu);
   SV_HIP(hipSetDevice(D.phys));
   int rc;
   if ((rc = ready_locked(D))) return rc;
-  rc = host_slice_locked(D, in, n, verdict, keys, path);
+  rc = host_slice_locked(D, in, n, verdict, keys, path, keys_cb, cb_ctx, cb_done);
   if (rc != SV_OK) {
     // leave the slot reusable: nothing of this call may still be in flight
     (void)hipStreamSynchronize(D.h2d);
@@ -669,8 +693,13 @@ int debug_fail() {
   return SV_OK;
 }
 
-int verify_host(const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, const sv_opts* opts) {
-  if (n == 0) return check_opts(opts);
+int verify_host(const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, const sv_opts* opts,
+                KeysReadyFn keys_cb = nullptr, void* cb_ctx = nullptr) {
+  if (n == 0) {
+    int rc = check_opts(opts);
+    if (rc == SV_OK && keys_cb) keys_cb(cb_ctx);
+    return rc;
+  }
   if (!verdict && !keys) return fail(SV_ERR_INVALID_ARG, "null buffer");
   int rc = check_msgs(in, n);
   if (rc) return rc;
@@ -679,10 +708,17 @@ int verify_host(const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, con
   std::vector<Device*> devs;
   if ((rc = select_devices(opts, n, devs))) return rc;
   const int path = path_from_flags(opts ? opts->flags : 0u);
-  return shard(devs, n, [&](Device& D, size_t lo, size_t hi) {
-    return host_slice(D, in.sub(lo), hi - lo, verdict ? verdict + lo : nullptr, keys ? keys + 32 * lo : nullptr,
-                      path);
-  });
+  bool cb_done = false;
+  if (devs.size() == 1) {
+    rc = host_slice(*devs[0], in, n, verdict, keys, path, keys_cb, cb_ctx, &cb_done);
+  } else {
+    rc = shard(devs, n, [&](Device& D, size_t lo, size_t hi) {
+      return host_slice(D, in.sub(lo), hi - lo, verdict ? verdict + lo : nullptr, keys ? keys + 32 * lo : nullptr,
+                        path);
+    });
+  }
+  if (rc == SV_OK && keys_cb && !cb_done) keys_cb(cb_ctx);  // (keys complete; no overlap possible)
+  return rc;
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -774,6 +810,18 @@ int sv_ed25519_verify_batch_gather(const uint8_t* const* pk, const uint8_t* cons
   in.pmsg = msg;
   in.len = msg_len;
   return verify_host(in, n, verdict, keys, opts);
+}
+
+int sv_ed25519_verify_batch_gather_cb(const uint8_t* const* pk, const uint8_t* const* sig,
+                                      const uint8_t* const* msg, const uint32_t* msg_len, size_t n, uint8_t* verdict,
+                                      uint8_t* keys, void (*keys_ready)(void* ctx), void* ctx, const sv_opts* opts) {
+  if (n && (!pk || !verdict || !keys || !keys_ready)) return fail(SV_ERR_INVALID_ARG, "null buffer");
+  HostIn in;
+  in.ppk = pk;
+  in.psig = sig;
+  in.pmsg = msg;
+  in.len = msg_len;
+  return verify_host(in, n, verdict, keys, opts, keys_ready, ctx);
 }
 
 int sv_ed25519_verify_batch_keyed(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,

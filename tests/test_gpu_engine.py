@@ -257,11 +257,16 @@ def test_forced_engine_error_falls_back_to_cpu_path(sv, dev, golden, keyed):
         with pytest.raises(sv.SigVerifyError):
             sv.verify_batch(d["pk"][:10], d["sig"][:10], d["msg"], d["msg_off"][:10], d["msg_len"][:10])
         host.svh_cache_clear()
+        host.svh_cache_counts(None, None)
         _stats(host)
         out = _svh_batch(host, d, np.arange(len(d["verdict"])))
         assert np.array_equal(out, d["verdict"])
         s = _stats(host)
-        assert s.fallbacks == 1 and s.gpu_signatures == 0 and s.cpu_signatures == len(d["verdict"])
+        h, m = ctypes.c_uint64(), ctypes.c_uint64()
+        host.svh_cache_counts(ctypes.byref(h), ctypes.byref(m))
+        # keyed: every eligible row re-run on the CPU; else the distinct misses
+        want_cpu = len(d["verdict"]) if keyed else m.value
+        assert s.fallbacks == 1 and s.gpu_signatures == 0 and s.cpu_signatures == want_cpu
     finally:
         sv.set_debug_flags(prev)
         host.svh_set_keyed_threshold(256)

@@ -44,7 +44,7 @@ int main(int argc, char** argv) {
     for (auto& b : msgs[i]) b = (uint8_t)rng();
   }
   std::vector<PubKeyUtils::VerifyItem> items(n);
-  for (size_t i = 0; i < n; ++i) items[i] = PubKeyUtils::VerifyItem{&keys[i], &sigs[i], ByteSlice(msgs[i])};
+  for (size_t i = 0; i < n; ++i) items[i] = PubKeyUtils::VerifyItem{&keys[i], ByteSlice(sigs[i]), ByteSlice(msgs[i])};
 
   auto time = [&](const char* what, auto fn, int reps = 3) {
     double best = 1e9;
@@ -121,8 +121,8 @@ int main(int argc, char** argv) {
         th.emplace_back([&, p] {
           std::vector<std::future<bool>> f;
           for (size_t i = p; i < n; i += 8) {
-            if (post) mb.post(keys[i], sigs[i], ByteSlice(msgs[i]));
-            else f.push_back(mb.submit(keys[i], sigs[i], ByteSlice(msgs[i])));
+            if (post) mb.post(keys[i], ByteSlice(sigs[i]), ByteSlice(msgs[i]));
+            else f.push_back(mb.submit(keys[i], ByteSlice(sigs[i]), ByteSlice(msgs[i])));
           }
           for (auto& x : f) x.get();
         });
