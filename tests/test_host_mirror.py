@@ -631,6 +631,6 @@ def test_gpu_config3_full_5000_tx(host, sv, oracle):
         host.svh_cache_clear()
         ok, used, pairs = _check(host, txs, mode)
         assert (ok == want_ok).all() and (used == want_used).all(), mode
-        assert pairs > 40000
+        assert pairs > 25000  # (~5.8 signatures per tx on average)
     assert 0 < want_ok.sum() < len(txs)
     host.svh_cache_clear()

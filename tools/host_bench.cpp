@@ -108,6 +108,36 @@ int main(int argc, char** argv) {
     });
   }
 
+  if (gpu) {
+    // per-batch latency of the keyed path at micro-batcher sizes
+    for (size_t b : {1024, 4096, 16384}) {
+      std::vector<PubKeyUtils::VerifyItem> sub(items.begin(), items.begin() + b);
+      PubKeyUtils::verifySigBatch(sub);
+      double best = 1e9;
+      for (int r = 0; r < 20; ++r) {
+        PubKeyUtils::clearVerifySigCache();
+        auto t0 = clk::now();
+        PubKeyUtils::verifySigBatch(sub);
+        best = std::min(best, std::chrono::duration<double>(clk::now() - t0).count());
+      }
+      printf("verifySigBatch keyed (GPU) one batch of %-6zu                  %8.3f ms\n", b, best * 1e3);
+    }
+    for (unsigned workers : {1u, 2u, 4u})
+      for (size_t mb_size : {1024, 4096, 16384}) {
+        char label[128];
+        snprintf(label, sizeof label, "micro-batcher (GPU) post, 8 producers, %u workers, %zu/batch", workers, mb_size);
+        time(label, [&] {
+          VerifyMicroBatcher mb(mb_size, std::chrono::microseconds(1000), workers);
+          std::vector<std::thread> th;
+          for (int p = 0; p < 8; ++p)
+            th.emplace_back([&, p] {
+              for (size_t i = p; i < n; i += 8) mb.post(keys[i], ByteSlice(sigs[i]), ByteSlice(msgs[i]));
+            });
+          for (auto& t : th) t.join();
+          mb.drain();
+        });
+      }
+  }
   for (int post = 0; post < 2; ++post) {
     PubKeyUtils::setBatchVerifierForTesting(nullptr);
     PubKeyUtils::setKeyedBatchVerifierForTesting(gpu ? nullptr : stub_keyed);
