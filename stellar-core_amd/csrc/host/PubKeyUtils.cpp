@@ -173,18 +173,26 @@ class RandomEvictionCache {
     ordGen_[e.pos] = ++generation_;
     return e;
   }
-  // put(); owner != 0 inserts a pending value
-  void put(Hash const& k, bool v, uint64_t owner = 0, uint32_t pendIdx = 0) {
-    ++generation_;
+  // put(); owner != 0 inserts a pending value.  Returns the entry id.
+  uint32_t put(Hash const& k, bool v, uint64_t owner = 0, uint32_t pendIdx = 0) {
     const uint32_t id = find(k);
     if (id != kNone) {
-      Entry& e = entries_[id];
-      ordGen_[e.pos] = generation_;
-      e.value = v;
-      e.owner = owner;
-      e.pendIdx = pendIdx;
-      return;
+      update(id, v, owner, pendIdx);
+      return id;
     }
+    return insertNew(k, v, owner, pendIdx);
+  }
+  // put() of a key find() just reported present (id) ...
+  void update(uint32_t id, bool v, uint64_t owner, uint32_t pendIdx) {
+    Entry& e = entries_[id];
+    ordGen_[e.pos] = ++generation_;
+    e.value = v;
+    e.owner = owner;
+    e.pendIdx = pendIdx;
+  }
+  // ... or absent (the caller's find() returned kNone)
+  uint32_t insertNew(Hash const& k, bool v, uint64_t owner, uint32_t pendIdx) {
+    ++generation_;
     const uint32_t pos = (uint32_t)ordId_.size();
     uint32_t nid;
     if (!freeIds_.empty()) {
@@ -202,17 +210,18 @@ class RandomEvictionCache {
     ordGen_.push_back(generation_);
     if (ordId_.size() > maxSize_) evictOne();
     if (!freeIds_.empty()) __builtin_prefetch(&entries_[freeIds_.back()], 1);  // the next insert's slot
+    return nid;
   }
-  // fills in a pending value if the entry is still this batch's
-  void resolve(Hash const& k, uint64_t owner, uint32_t pendIdx, bool v) {
-    const uint32_t id = find(k);
-    if (id == kNone) return;
+  // fills in a pending value if entry `id` still holds this batch's item (it
+  // may have been evicted and its id reused since)
+  void resolve(uint32_t id, uint64_t owner, uint32_t pendIdx, bool v) {
     Entry& e = entries_[id];
     if (e.owner == owner && e.pendIdx == pendIdx) {
       e.value = v;
       e.owner = 0;
     }
   }
+  void prefetchEntry(uint32_t id) const { __builtin_prefetch(&entries_[id], 1); }
   void clear() {
     std::fill(table_.begin(), table_.end(), 0u);
     entries_.clear();
@@ -331,7 +340,7 @@ struct Scratch {
   std::vector<size_t> rows, missRows, missItems;
   std::vector<Hash> keys;
   std::vector<uint8_t> verdict, mv;
-  std::vector<uint32_t> ref;
+  std::vector<uint32_t> ref, ids;
   std::vector<const uint8_t*> pk, sig, msg;
   std::vector<uint32_t> len;
   // SoA copy for the test hooks (the engine itself gathers)
@@ -468,8 +477,11 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     // cache walk (phase 1: hits, misses inserted pending in item order) runs
     // as soon as the keys are back, overlapping the GPU's verification; the
     // pending values are filled in once the verdicts arrive (phase 3).
+    constexpr uint32_t kNone = RandomEvictionCache::kNone;
     std::vector<uint8_t>& hit = sc.mv;
     hit.assign(E, 0);
+    std::vector<uint32_t>& pid = sc.ref;  // entry id of each pending insert
+    pid.assign(E, kNone);
     uint64_t owner = 0;
     bool walked = false;
     std::function<void()> phase1 = [&] {
@@ -478,7 +490,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
       for (size_t e = 0; e < E; ++e) {
         if (e + 8 < E) gVerifySigCache.prefetch(keys[e + 8]);
         const uint32_t id = gVerifySigCache.find(keys[e]);
-        if (id != RandomEvictionCache::kNone) {
+        if (id != kNone) {
           auto const& ent = gVerifySigCache.at(id);
           if (ent.owner == 0 || ent.owner == owner) {  // cached, or an earlier item of this batch
             ++gVerifyCacheHit;
@@ -489,9 +501,13 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
             }
             continue;
           }
+          ++gVerifyCacheMiss;  // another batch's pending entry: put() over it
+          gVerifySigCache.update(id, false, owner, (uint32_t)e);
+          pid[e] = id;
+          continue;
         }
         ++gVerifyCacheMiss;
-        gVerifySigCache.put(keys[e], false, owner, (uint32_t)e);
+        pid[e] = gVerifySigCache.insertNew(keys[e], false, owner, (uint32_t)e);
       }
       walked = true;
     };
@@ -509,8 +525,10 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     if (!walked) phase1();  // (not reached: the engine ran it on success)
     {
       std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
-      for (size_t e = 0; e < E; ++e)
-        if (!hit[e]) gVerifySigCache.resolve(keys[e], owner, (uint32_t)e, verdict[e] != 0);
+      for (size_t e = 0; e < E; ++e) {
+        if (e + 8 < E && pid[e + 8] != kNone) gVerifySigCache.prefetchEntry(pid[e + 8]);
+        if (pid[e] != kNone) gVerifySigCache.resolve(pid[e], owner, (uint32_t)e, verdict[e] != 0);
+      }
     }
     for (size_t e = 0; e < E; ++e)
       if (!hit[e]) out[rows[e]] = verdict[e] != 0;
@@ -521,6 +539,8 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     missRows.clear();
     std::vector<uint32_t>& ref = sc.ref;
     ref.assign(E, RandomEvictionCache::kNone);
+    std::vector<uint32_t>& missIds = sc.ids;  // entry id of each pending insert
+    missIds.clear();
     uint64_t owner;
     {
       std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
@@ -543,7 +563,8 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
         }
         ++gVerifyCacheMiss;
         ref[e] = (uint32_t)missRows.size();
-        gVerifySigCache.put(keys[e], false, owner, ref[e]);
+        missIds.push_back(id != RandomEvictionCache::kNone ? (gVerifySigCache.update(id, false, owner, ref[e]), id)
+                                                           : gVerifySigCache.insertNew(keys[e], false, owner, ref[e]));
         missRows.push_back(e);
       }
     }
@@ -568,7 +589,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     // phase 3: fill in the pending values
     {
       std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
-      for (size_t m = 0; m < M; ++m) gVerifySigCache.resolve(keys[missRows[m]], owner, (uint32_t)m, mv[m] != 0);
+      for (size_t m = 0; m < M; ++m) gVerifySigCache.resolve(missIds[m], owner, (uint32_t)m, mv[m] != 0);
     }
     for (size_t e = 0; e < E; ++e)
       if (ref[e] != RandomEvictionCache::kNone) out[rows[e]] = mv[ref[e]] != 0;

@@ -7,10 +7,16 @@
 
 namespace stellar {
 
+namespace {
+int64_t nowNs() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+}  // namespace
+
 VerifyMicroBatcher::VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay, unsigned workers,
                                        bool recordLatency)
     : mMaxBatch(std::max<size_t>(1, maxBatch)), mMaxDelay(maxDelay), mRecordLatency(recordLatency) {
-  mQ.recs.reserve(mMaxBatch);
   const unsigned w = std::max(1u, workers);
   mWorkers.reserve(w);
   for (unsigned i = 0; i < w; ++i) mWorkers.emplace_back([this] { run(); });
@@ -25,30 +31,40 @@ VerifyMicroBatcher::~VerifyMicroBatcher() {
   for (auto& w : mWorkers) w.join();
 }
 
+void VerifyMicroBatcher::wake() {
+  { std::lock_guard<std::mutex> g(mMu); }  // a worker between its check and its wait cannot miss this
+  mCv.notify_one();
+}
+
 void VerifyMicroBatcher::enqueue(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg,
                                  std::promise<bool>* done) {
+  // each producer thread keeps to one shard
+  thread_local unsigned tShard = ~0u;
+  if (tShard == ~0u) tShard = mNextShard.fetch_add(1) % kShards;
   Rec r;
   r.key = key;
-  // a signature longer than 64 bytes is not an XDR Signature; anything but 64
-  // is rejected by verifySig before verification, so keep at most 64 bytes
-  // and the real size
+  // anything but a 64-byte signature is rejected by verifySig before it is
+  // read; keep at most 64 bytes and the size (clamped to 65)
   r.sigLen = (uint32_t)std::min<size_t>(sig.size(), 65);
   std::memcpy(r.sig, sig.data(), std::min<size_t>(sig.size(), 64));
   r.msgLen = (uint32_t)msg.size();
   r.done = done;
   if (mRecordLatency) r.t0 = Clock::now();
-  bool wake;
   {
-    std::lock_guard<std::mutex> g(mMu);
-    if (mQ.recs.empty()) mOldest = mRecordLatency ? r.t0 : Clock::now();
-    r.msgOff = mQ.arena.size();
-    mQ.arena.insert(mQ.arena.end(), msg.begin(), msg.end());
-    mQ.recs.push_back(r);
-    ++mStats.items;
-    ++mEnqueued;
-    wake = mQ.recs.size() == 1 || mQ.recs.size() == mMaxBatch;
+    Shard& sh = mShards[tShard];
+    std::lock_guard<std::mutex> g(sh.mu);
+    r.msgOff = sh.q.arena.size();
+    sh.q.arena.insert(sh.q.arena.end(), msg.begin(), msg.end());
+    sh.q.recs.push_back(r);
   }
-  if (wake) mCv.notify_one();
+  mEnqueued.fetch_add(1);
+  const size_t q = mQueued.fetch_add(1) + 1;
+  if (q == 1) {
+    mOldestNs.store(nowNs());
+    wake();
+  } else if (q == mMaxBatch) {
+    wake();
+  }
 }
 
 std::future<bool> VerifyMicroBatcher::submit(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg) {
@@ -64,7 +80,7 @@ void VerifyMicroBatcher::post(PublicKey const& key, ByteSlice const& sig, ByteSl
 
 void VerifyMicroBatcher::drain() {
   std::unique_lock<std::mutex> lk(mMu);
-  const uint64_t target = mEnqueued;
+  const uint64_t target = mEnqueued.load();
   mCv.notify_all();
   mDoneCv.wait(lk, [&] { return mCompleted >= target; });
 }
@@ -79,49 +95,75 @@ std::vector<double> VerifyMicroBatcher::latencies() const {
   return mLatUs;
 }
 
+size_t VerifyMicroBatcher::takeFrom(size_t s, size_t want, Queue& into) {
+  Shard& sh = mShards[s];
+  std::lock_guard<std::mutex> g(sh.mu);
+  Queue& q = sh.q;
+  const size_t n = q.recs.size();
+  if (n == 0 || want == 0) return 0;
+  into.recs.clear();
+  into.arena.clear();
+  if (n <= want) {
+    std::swap(into, q);  // the whole sub-queue, no copy
+    return n;
+  }
+  const uint64_t cut = q.recs[want].msgOff;  // the oldest `want` items; the rest stay (offsets rebased)
+  into.recs.assign(q.recs.begin(), q.recs.begin() + want);
+  into.arena.assign(q.arena.begin(), q.arena.begin() + cut);
+  q.recs.erase(q.recs.begin(), q.recs.begin() + want);
+  q.arena.erase(q.arena.begin(), q.arena.begin() + cut);
+  for (Rec& r : q.recs) r.msgOff -= cut;
+  return want;
+}
+
 void VerifyMicroBatcher::run() {
-  std::unique_lock<std::mutex> lk(mMu);
-  Queue batch;
+  std::vector<Queue> parts(kShards);
   std::vector<PubKeyUtils::VerifyItem> items;
+  std::vector<Rec const*> recs;
   std::vector<double> lat;
+  size_t start = 0;
+  std::unique_lock<std::mutex> lk(mMu);
   for (;;) {
     // wait for: stop, a full batch, or the oldest item's deadline
-    while (!mStop && mQ.recs.empty()) mCv.wait(lk);
-    if (mQ.recs.empty()) return;  // stop requested and the queue is drained
-    if (mQ.recs.size() < mMaxBatch && !mStop) {
-      const auto deadline = mOldest + mMaxDelay;
-      if (Clock::now() < deadline) {
-        mCv.wait_until(lk, deadline, [&] { return mStop || mQ.recs.size() >= mMaxBatch; });
+    while (!mStop && mQueued.load() == 0) mCv.wait(lk);
+    if (mQueued.load() == 0) return;  // stop requested and every queue drained
+    if (mQueued.load() < mMaxBatch && !mStop) {
+      const int64_t deadline = mOldestNs.load() + (int64_t)mMaxDelay.count() * 1000;
+      const int64_t now = nowNs();
+      if (now < deadline) {
+        mCv.wait_for(lk, std::chrono::nanoseconds(deadline - now),
+                     [&] { return mStop || mQueued.load() >= mMaxBatch; });
         continue;  // re-evaluate: another worker may have taken the queue meanwhile
       }
     }
-    const bool bySize = mQ.recs.size() >= mMaxBatch;
-    batch.recs.clear();
-    batch.arena.clear();
-    if (mQ.recs.size() <= mMaxBatch) {
-      std::swap(batch, mQ);  // the whole queue, no copy
-    } else {
-      // the oldest maxBatch items; the rest stay queued (offsets rebased)
-      const uint64_t cut = mQ.recs[mMaxBatch].msgOff;
-      batch.recs.assign(mQ.recs.begin(), mQ.recs.begin() + mMaxBatch);
-      batch.arena.assign(mQ.arena.begin(), mQ.arena.begin() + cut);
-      mQ.recs.erase(mQ.recs.begin(), mQ.recs.begin() + mMaxBatch);
-      mQ.arena.erase(mQ.arena.begin(), mQ.arena.begin() + cut);
-      for (Rec& r : mQ.recs) r.msgOff -= cut;
-      mOldest = Clock::now();  // (the remaining items arrived no earlier than the flush decision)
-      mCv.notify_one();        // leftovers: another worker can take them
-    }
-    const size_t take = batch.recs.size();
-    ++mStats.batches;
-    if (bySize) ++mStats.flushedBySize;
-    else ++mStats.flushedByDeadline;
-    mStats.maxBatchSeen = std::max<uint64_t>(mStats.maxBatchSeen, take);
+    const bool bySize = mQueued.load() >= mMaxBatch;
     lk.unlock();
-    items.resize(take);
-    const uint8_t* arena = batch.arena.data();
-    for (size_t i = 0; i < take; ++i) {
-      Rec const& r = batch.recs[i];
-      items[i] = PubKeyUtils::VerifyItem{&r.key, ByteSlice(r.sig, r.sigLen), ByteSlice(arena + r.msgOff, r.msgLen)};
+    // collect up to maxBatch items, starting from a rotating shard
+    size_t take = 0;
+    for (size_t k = 0; k < kShards; ++k) {
+      const size_t s = (start + k) % kShards;
+      const size_t got = takeFrom(s, mMaxBatch - take, parts[s]);
+      if (got == 0) parts[s].recs.clear();
+      take += got;
+    }
+    start = (start + 1) % kShards;
+    const size_t left = mQueued.fetch_sub(take) - take;
+    if (left > 0) {
+      mOldestNs.store(nowNs());  // (an upper bound for the leftovers' arrival)
+      if (left >= mMaxBatch) wake();
+    }
+    if (take == 0) {
+      lk.lock();
+      continue;
+    }
+    items.clear();
+    recs.clear();
+    for (size_t s = 0; s < kShards; ++s) {
+      const uint8_t* arena = parts[s].arena.data();
+      for (Rec const& r : parts[s].recs) {
+        items.push_back(PubKeyUtils::VerifyItem{&r.key, ByteSlice(r.sig, r.sigLen), ByteSlice(arena + r.msgOff, r.msgLen)});
+        recs.push_back(&r);
+      }
     }
     bool ok = true;
     try {
@@ -129,23 +171,27 @@ void VerifyMicroBatcher::run() {
       if (mRecordLatency) {
         const auto now = Clock::now();
         lat.resize(take);
-        for (size_t i = 0; i < take; ++i)
-          lat[i] = std::chrono::duration<double, std::micro>(now - batch.recs[i].t0).count();
+        for (size_t i = 0; i < take; ++i) lat[i] = std::chrono::duration<double, std::micro>(now - recs[i]->t0).count();
       }
       for (size_t i = 0; i < take; ++i)
-        if (std::promise<bool>* p = batch.recs[i].done) {
+        if (std::promise<bool>* p = recs[i]->done) {
           p->set_value(v[i]);
           delete p;
         }
     } catch (...) {  // (only a non-ed25519 key: the reference's releaseAssert)
       ok = false;
       for (size_t i = 0; i < take; ++i)
-        if (std::promise<bool>* p = batch.recs[i].done) {
+        if (std::promise<bool>* p = recs[i]->done) {
           p->set_exception(std::current_exception());
           delete p;
         }
     }
     lk.lock();
+    ++mStats.batches;
+    if (bySize) ++mStats.flushedBySize;
+    else ++mStats.flushedByDeadline;
+    mStats.items += take;
+    mStats.maxBatchSeen = std::max<uint64_t>(mStats.maxBatchSeen, take);
     if (ok && mRecordLatency) {
       for (size_t i = 0; i < take; ++i) {
         if (mLatUs.size() < kLatencySamples) mLatUs.push_back(lat[i]);

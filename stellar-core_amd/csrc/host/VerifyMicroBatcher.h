@@ -14,15 +14,19 @@
 // overlaps another's engine call.  The engine and the verify cache are
 // thread-safe, so verdicts do not depend on the worker count.
 //
-// Queue layout: fixed records (key, signature bytes) plus one byte arena for
-// the messages; a flushing worker swaps the whole queue out under the lock, so
-// enqueueing costs one short critical section and no allocation per item
-// (submit() allocates its promise).
+// Queue layout: kShards sub-queues, each fixed records (key, signature
+// bytes) plus one byte arena for the messages under its own mutex; a producer
+// thread always appends to "its" shard (so concurrent producers rarely share a
+// lock) and a flushing worker swaps whole sub-queues out, so enqueueing is one
+// short uncontended critical section and no allocation per item (submit()
+// allocates its promise).  Item order inside a batch follows the shards;
+// verdicts do not depend on it.
 //
 // Engine errors never reach producers: verifySigBatch re-runs a failed batch
 // on the CPU path (PubKeyUtils.h).
 #pragma once
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -72,27 +76,38 @@ class VerifyMicroBatcher {
     uint8_t sig[64];
     uint32_t sigLen;
     uint32_t msgLen;
-    uint64_t msgOff;                // into the arena
-    std::promise<bool>* done;       // submit() only
-    Clock::time_point t0;           // recordLatency only
+    uint64_t msgOff;           // into the arena
+    std::promise<bool>* done;  // submit() only
+    Clock::time_point t0;      // recordLatency only
   };
   struct Queue {
     std::vector<Rec> recs;
     std::vector<uint8_t> arena;
   };
+  static constexpr size_t kShards = 8;
+  struct alignas(64) Shard {
+    std::mutex mu;
+    Queue q;
+  };
   void enqueue(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg, std::promise<bool>* done);
+  void wake();
+  // moves up to `want` of the oldest items of shard s into `into`; returns the count
+  size_t takeFrom(size_t s, size_t want, Queue& into);
   void run();
 
   const size_t mMaxBatch;
   const std::chrono::microseconds mMaxDelay;
   const bool mRecordLatency;
-  mutable std::mutex mMu;
+  Shard mShards[kShards];
+  std::atomic<size_t> mQueued{0};
+  std::atomic<int64_t> mOldestNs{0};   // arrival (steady_clock ns) of the oldest queued item
+  std::atomic<uint64_t> mEnqueued{0};
+  std::atomic<unsigned> mNextShard{0};
+  mutable std::mutex mMu;  // worker wake-ups, stats, drain
   std::condition_variable mCv;
   std::condition_variable mDoneCv;
-  Queue mQ;
-  Clock::time_point mOldest;  // arrival of the oldest queued item
   bool mStop = false;
-  uint64_t mEnqueued = 0, mCompleted = 0;
+  uint64_t mCompleted = 0;
   Stats mStats;
   std::vector<double> mLatUs;  // ring of kLatencySamples
   size_t mLatNext = 0;
