@@ -6,7 +6,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <functional>
 #include <limits>
 #include <mutex>
@@ -331,6 +334,7 @@ std::atomic<PubKeyUtils::BatchVerifyFn> gTestVerifier{nullptr};
 std::atomic<PubKeyUtils::KeyedBatchVerifyFn> gTestKeyedVerifier{nullptr};
 std::atomic<size_t> gKeyedThreshold{256};
 std::atomic<size_t> gCpuThreshold{1};
+const bool gTrace = getenv("SV_HOST_TRACE") != nullptr;  // stage timings of keyed batches to stderr
 
 using Item = PubKeyUtils::VerifyItem;
 
@@ -511,9 +515,25 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
       }
       walked = true;
     };
+    const bool trace = gTrace;
+    const auto tA = std::chrono::steady_clock::now();
+    std::chrono::steady_clock::time_point tB{}, tC{};
+    std::function<void()> walk = phase1;
+    if (trace)
+      phase1 = [&] {
+        tB = std::chrono::steady_clock::now();
+        walk();
+        tC = std::chrono::steady_clock::now();
+      };
     if (gpuVerify(items, rows, verdict.data(), keys.data(), &phase1) == SV_OK) {
       gGpuSigs += E;
       gGpuBatches += 1;
+      if (trace) {
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        const auto tD = std::chrono::steady_clock::now();
+        fprintf(stderr, "[verifySigBatch keyed n=%zu] keys ready %.3f ms, walk %.3f ms, verdicts %.3f ms after walk\n",
+                E, ms(tA, tB), ms(tB, tC), ms(tC, tD));
+      }
     } else {
       ++gFallbacks;
       if (!walked) {

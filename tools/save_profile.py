@@ -4,7 +4,7 @@
   python tools/save_profile.py gpurun_out/r1b/prof profiles/r01/<name>
 
 Copies the kernel-stats and counter CSVs plus summary.json, and rewrites
-profiles/r01_traffic.json (the file bench.py reads roofline.traffic from,
+profiles/r02_traffic.json (the file bench.py reads roofline.traffic from,
 keyed by the verify kernel's source digest) from the summary.
 """
 import glob
@@ -40,7 +40,7 @@ def main():
         "kernel": s["kernel"],
         "kernel_source_sha256": s["kernel_source_sha256"],
     }
-    with open(os.path.join(repo, "profiles", "r01_traffic.json"), "w") as f:
+    with open(os.path.join(repo, "profiles", "r02_traffic.json"), "w") as f:
         json.dump(t, f, indent=1)
     print(json.dumps(t, indent=1))
 
