@@ -4,9 +4,10 @@
 // (limb i has weight 2^ceil(25.5 i): offsets 0,26,51,77,102,128,153,179,204,230;
 // even limbs 26 bits, odd limbs 25 bits when carried).
 //
-// Why this and not 8 x 32-bit limbs: the microbenchmark in
-// profiles/r01_ubench_imul.txt shows v_mad_u64_u32 issues at the same rate as
-// v_add_co_u32 on gfx950, so cost = instruction count.  With 25.5-bit limbs
+// Why this and not 8 x 32-bit limbs: on gfx950 v_mad_u64_u32 issues at the
+// same rate as the carry-propagating v_add_co_u32 / v_addc_co_u32 (4.8 SIMD
+// cycles per wave-instruction at 2 waves/SIMD, profiles/r02/ubench_valu_rates.txt),
+// so cost = instruction count.  With 25.5-bit limbs
 // every product-accumulate is ONE v_mad_u64_u32 into a carry-free 64-bit column
 // sum (no per-product carry flags, no realignment of 64-bit register pairs),
 // followed by a single carry chain per multiply.
@@ -217,30 +218,235 @@ SV_HD void fe_sq_cols(uint64_t h[10], const fe& f) {
   }
 }
 
+// Column-major forms with the carry chain folded into the multiply-adds:
+// column k (terms i + j = k and i + j = k + 10) is opened by a mad whose
+// addend is the carry out of column k - 1, so each carry step is one 64-bit
+// shift and one mask; the separate 64-bit add of fe_carry_wide is gone (9 of
+// them per product).  The price is one dependent chain per product instead of
+// ten interleaved accumulators.  Bounds: the carry (< 2^38) adds nothing
+// measurable to a column sum (< 2^62.8), and the output is R as above.
+#ifndef SV_COLMAJOR
+#define SV_COLMAJOR 1
+#endif
+// One column as ONE inline-asm statement (z: the first mad opens with 0, a:
+// with acc).  Per-mad statements cost an s_nop between every two dependent
+// ones: LLVM's gfx950 hazard recognizer assumes any inline asm may carry the
+// dst-sel forwarding hazard (16-bit SDWA / op_sel destinations), which
+// v_mad_u64_u32 does not have, and pads a consumer statement by one wait
+// state.  Inside one statement the mads issue back to back; a dependent chain
+// costs nothing extra on gfx950 (tools/ubench_valu_rates: dependency distance
+// 1, 2 and 4 issue at the independent rate).
+#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
+SV_HD void sv_col10_z(uint64_t& acc, const uint32_t a[10], const uint32_t b[10]) {
+  asm(
+      "v_mad_u64_u32 %0, s[94:95], %1, %11, 0\n"
+      "v_mad_u64_u32 %0, s[92:93], %2, %12, %0\n"
+      "v_mad_u64_u32 %0, s[90:91], %3, %13, %0\n"
+      "v_mad_u64_u32 %0, s[88:89], %4, %14, %0\n"
+      "v_mad_u64_u32 %0, s[94:95], %5, %15, %0\n"
+      "v_mad_u64_u32 %0, s[92:93], %6, %16, %0\n"
+      "v_mad_u64_u32 %0, s[90:91], %7, %17, %0\n"
+      "v_mad_u64_u32 %0, s[88:89], %8, %18, %0\n"
+      "v_mad_u64_u32 %0, s[94:95], %9, %19, %0\n"
+      "v_mad_u64_u32 %0, s[92:93], %10, %20, %0\n"
+      : "=&v"(acc)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]), "v"(a[9]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]), "v"(b[8]), "v"(b[9])
+      : "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95");
+}
+SV_HD void sv_col10_a(uint64_t& acc, const uint32_t a[10], const uint32_t b[10]) {
+  asm(
+      "v_mad_u64_u32 %0, s[94:95], %1, %11, %0\n"
+      "v_mad_u64_u32 %0, s[92:93], %2, %12, %0\n"
+      "v_mad_u64_u32 %0, s[90:91], %3, %13, %0\n"
+      "v_mad_u64_u32 %0, s[88:89], %4, %14, %0\n"
+      "v_mad_u64_u32 %0, s[94:95], %5, %15, %0\n"
+      "v_mad_u64_u32 %0, s[92:93], %6, %16, %0\n"
+      "v_mad_u64_u32 %0, s[90:91], %7, %17, %0\n"
+      "v_mad_u64_u32 %0, s[88:89], %8, %18, %0\n"
+      "v_mad_u64_u32 %0, s[94:95], %9, %19, %0\n"
+      "v_mad_u64_u32 %0, s[92:93], %10, %20, %0\n"
+      : "+v"(acc)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]), "v"(a[9]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]), "v"(b[8]), "v"(b[9])
+      : "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95");
+}
+SV_HD void sv_col6_z(uint64_t& acc, const uint32_t a[6], const uint32_t b[6]) {
+  asm(
+      "v_mad_u64_u32 %0, s[94:95], %1, %7, 0\n"
+      "v_mad_u64_u32 %0, s[92:93], %2, %8, %0\n"
+      "v_mad_u64_u32 %0, s[90:91], %3, %9, %0\n"
+      "v_mad_u64_u32 %0, s[88:89], %4, %10, %0\n"
+      "v_mad_u64_u32 %0, s[94:95], %5, %11, %0\n"
+      "v_mad_u64_u32 %0, s[92:93], %6, %12, %0\n"
+      : "=&v"(acc)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5])
+      : "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95");
+}
+SV_HD void sv_col6_a(uint64_t& acc, const uint32_t a[6], const uint32_t b[6]) {
+  asm(
+      "v_mad_u64_u32 %0, s[94:95], %1, %7, %0\n"
+      "v_mad_u64_u32 %0, s[92:93], %2, %8, %0\n"
+      "v_mad_u64_u32 %0, s[90:91], %3, %9, %0\n"
+      "v_mad_u64_u32 %0, s[88:89], %4, %10, %0\n"
+      "v_mad_u64_u32 %0, s[94:95], %5, %11, %0\n"
+      "v_mad_u64_u32 %0, s[92:93], %6, %12, %0\n"
+      : "+v"(acc)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5])
+      : "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95");
+}
+SV_HD void sv_col5_a(uint64_t& acc, const uint32_t a[5], const uint32_t b[5]) {
+  asm(
+      "v_mad_u64_u32 %0, s[94:95], %1, %6, %0\n"
+      "v_mad_u64_u32 %0, s[92:93], %2, %7, %0\n"
+      "v_mad_u64_u32 %0, s[90:91], %3, %8, %0\n"
+      "v_mad_u64_u32 %0, s[88:89], %4, %9, %0\n"
+      "v_mad_u64_u32 %0, s[94:95], %5, %10, %0\n"
+      : "+v"(acc)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4])
+      : "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95");
+}
+#endif
+
+// limb 0 receives 19 * (carry out of limb 9), then one carry into limb 1
+SV_HD void fe_carry_wrap(fe& out, uint64_t c9) {
+  const uint64_t h0 = (uint64_t)out.v[0] + c9 * 19u;
+  out.v[0] = (uint32_t)h0 & SV_M26;
+  out.v[1] += (uint32_t)(h0 >> 26);
+}
+// opens column k: the carry of column k - 1 as the addend (k > 0)
+SV_HD void sv_mad_open(uint64_t& acc, uint64_t c, uint32_t a, uint32_t b, int k, int n) {
+  if (k == 0) {
+    sv_mad_init_k(acc, a, b, n);
+  } else {
+    acc = c;
+    sv_mad_k(acc, a, b, n);
+  }
+}
+SV_HD void sv_col_close(fe& out, uint64_t& c, uint64_t acc, int k) {
+  c = acc >> fe_width(k);
+  out.v[k] = (uint32_t)acc & fe_mask(k);
+}
+// (out may alias f or g: the limbs are written to a local first)
+template <bool DBL>
+SV_HD void fe_mul_cm(fe& h, const fe& f, const fe& g) {
+  fe out;
+  uint32_t g19[10], fa[10], fb[10];
+  SV_UNROLL for (int j = 0; j < 10; ++j) g19[j] = 19u * g.v[j];
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    fa[i] = DBL ? (f.v[i] << 1) : f.v[i];
+    fb[i] = DBL ? (f.v[i] << 2) : (f.v[i] << 1);
+  }
+  uint64_t acc = 0, c = 0;
+  SV_UNROLL for (int k = 0; k < 10; ++k) {
+#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
+    uint32_t A[10], B[10];
+    SV_UNROLL for (int i = 0; i < 10; ++i) {
+      const int j = (k - i + 10) % 10;
+      A[i] = ((i & 1) && (j & 1)) ? fb[i] : fa[i];
+      B[i] = (i + j >= 10) ? g19[j] : g.v[j];
+    }
+    if (k == 0) {
+      sv_col10_z(acc, A, B);
+    } else {
+      acc = c;
+      sv_col10_a(acc, A, B);
+    }
+#else
+    SV_UNROLL for (int i = 0; i < 10; ++i) {
+      const int j = (k - i + 10) % 10;
+      const uint32_t a = ((i & 1) && (j & 1)) ? fb[i] : fa[i];
+      const uint32_t b = (i + j >= 10) ? g19[j] : g.v[j];
+      if (i == 0) sv_mad_open(acc, c, a, b, k, 10 * k + i);
+      else sv_mad_k(acc, a, b, 10 * k + i);
+    }
+#endif
+    sv_col_close(out, c, acc, k);
+  }
+  fe_carry_wrap(out, c);
+  h = out;
+}
+template <bool DBL>
+SV_HD void fe_sq_cm(fe& h, const fe& f) {
+  fe out;
+  uint64_t acc = 0, c = 0;
+  int n = 0;
+  SV_UNROLL for (int k = 0; k < 10; ++k) {
+    bool first = true;
+    uint32_t A[6], B[6];
+    int t = 0;
+    SV_UNROLL for (int i = 0; i < 10; ++i) {
+      SV_UNROLL for (int j = i; j < 10; ++j) {
+        if ((i + j) % 10 != k) continue;
+        const int sh = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + (DBL ? 1 : 0);
+        const uint32_t a = f.v[i] << sh;
+        const uint32_t b = (i + j >= 10) ? 19u * f.v[j] : f.v[j];
+        A[t] = a;
+        B[t] = b;
+        ++t;
+#if !(defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM)
+        if (first) sv_mad_open(acc, c, a, b, k, n);
+        else sv_mad_k(acc, a, b, n);
+#endif
+        first = false;
+        ++n;
+      }
+    }
+#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
+    // columns hold 6 terms (k even) or 5 (k odd)
+    if (k == 0) {
+      sv_col6_z(acc, A, B);
+    } else {
+      acc = c;
+      if (k & 1) sv_col5_a(acc, A, B);
+      else sv_col6_a(acc, A, B);
+    }
+#endif
+    (void)first;
+    sv_col_close(out, c, acc, k);
+  }
+  fe_carry_wrap(out, c);
+  h = out;
+}
+
 SV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
+#if SV_COLMAJOR
+  fe_mul_cm<false>(h, f, g);
+#else
   uint64_t c[10];
   fe_mul_cols<false>(c, f, g);
   fe_carry_wide(h, c);
+#endif
   SV_FENCE();
 }
 // h = 2 f g (doubling folded into the operand; inputs must be <= R)
 SV_HD void fe_mul2(fe& h, const fe& f, const fe& g) {
+#if SV_COLMAJOR
+  fe_mul_cm<true>(h, f, g);
+#else
   uint64_t c[10];
   fe_mul_cols<true>(c, f, g);
   fe_carry_wide(h, c);
+#endif
   SV_FENCE();
 }
 SV_HD void fe_sq(fe& h, const fe& f) {
+#if SV_COLMAJOR
+  fe_sq_cm<false>(h, f);
+#else
   uint64_t c[10];
   fe_sq_cols<false>(c, f);
   fe_carry_wide(h, c);
+#endif
   SV_FENCE();
 }
 // h = 2 f^2 (input must be <= R)
 SV_HD void fe_sq2(fe& h, const fe& f) {
+#if SV_COLMAJOR
+  fe_sq_cm<true>(h, f);
+#else
   uint64_t c[10];
   fe_sq_cols<true>(c, f);
   fe_carry_wide(h, c);
+#endif
   SV_FENCE();
 }
 // n successive squarings (rolled loop: keeps the code object small)

@@ -97,6 +97,23 @@ struct Stamp {
 #define F_FMA64(i, P) "v_fma_f64 %" i ", %" i ", %16, %17\n"
 
 DEF_KERNEL(k_mad_u64_u32, uint64_t, F_MAD, "v"(a), "v"(b))
+// dependency distance 1 / 2 / 4: every mad accumulates into the result of the
+// previous (1) or second / fourth previous mad -- the latency a column-major
+// product (one dependent chain per column) exposes
+#define A16D1(F) F("0", SP0) F("0", SP1) F("0", SP2) F("0", SP3) F("0", SP4) F("0", SP5) F("0", SP6) F("0", SP7) \
+                 F("0", SP0) F("0", SP1) F("0", SP2) F("0", SP3) F("0", SP4) F("0", SP5) F("0", SP6) F("0", SP7)
+#define A16D2(F) F("0", SP0) F("1", SP1) F("0", SP2) F("1", SP3) F("0", SP4) F("1", SP5) F("0", SP6) F("1", SP7) \
+                 F("0", SP0) F("1", SP1) F("0", SP2) F("1", SP3) F("0", SP4) F("1", SP5) F("0", SP6) F("1", SP7)
+#define A16D4(F) F("0", SP0) F("1", SP1) F("2", SP2) F("3", SP3) F("0", SP4) F("1", SP5) F("2", SP6) F("3", SP7) \
+                 F("0", SP0) F("1", SP1) F("2", SP2) F("3", SP3) F("0", SP4) F("1", SP5) F("2", SP6) F("3", SP7)
+#define DEF_KERNEL_D(NAME, T, AF, F, INS...)                  \
+  KERNEL_HEAD(NAME, T)                                        \
+  asm volatile(AF(F) : OPS16 : INS : CLOB, "vcc");            \
+  asm volatile(AF(F) : OPS16 : INS : CLOB, "vcc");            \
+  KERNEL_TAIL(T)
+DEF_KERNEL_D(k_mad_dep1, uint64_t, A16D1, F_MAD, "v"(a), "v"(b))
+DEF_KERNEL_D(k_mad_dep2, uint64_t, A16D2, F_MAD, "v"(a), "v"(b))
+DEF_KERNEL_D(k_mad_dep4, uint64_t, A16D4, F_MAD, "v"(a), "v"(b))
 DEF_KERNEL(k_mad_u64_u32_vcc, uint64_t, F_MADVCC, "v"(a), "v"(b))
 DEF_KERNEL(k_add_co_u32, uint32_t, F_ADDCO, "v"(a), "v"(b))
 DEF_KERNEL(k_addc_co_u32, uint32_t, F_ADDC, "v"(a), "v"(b))
@@ -151,6 +168,9 @@ int main(int argc, char** argv) {
             {"v_fma_f64", k_fma_f64, 1},
             {"v_mad_u64_u32 (8 rotating sdst pairs)", k_mad_u64_u32, 1},
             {"v_mad_u64_u32 (sdst vcc every inst)", k_mad_u64_u32_vcc, 1},
+            {"v_mad_u64_u32 dependency distance 1", k_mad_dep1, 1},
+            {"v_mad_u64_u32 dependency distance 2", k_mad_dep2, 1},
+            {"v_mad_u64_u32 dependency distance 4", k_mad_dep4, 1},
             {"v_mul_lo_u32", k_mul_lo_u32, 1},
             {"v_mul_hi_u32", k_mul_hi_u32, 1},
             {"v_add_u32", k_add_u32, 1},
