@@ -306,6 +306,19 @@ SV_HD void sv_col5_a(uint64_t& acc, const uint32_t a[5], const uint32_t b[5]) {
 }
 #endif
 
+// 2x as v_add_u32 x, x: LLVM canonicalises x + x to a shift, and gfx950
+// issues 32-bit shifts at half the rate of adds (tools/ubench_valu_rates:
+// 4.5 vs 2.6 SIMD cycles per wave-instruction at 2 waves/SIMD).
+SV_HD uint32_t sv_twice(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
+  return r;
+#else
+  return x << 1;
+#endif
+}
+
 // limb 0 receives 19 * (carry out of limb 9), then one carry into limb 1
 SV_HD void fe_carry_wrap(fe& out, uint64_t c9) {
   const uint64_t h0 = (uint64_t)out.v[0] + c9 * 19u;
@@ -332,8 +345,8 @@ SV_HD void fe_mul_cm(fe& h, const fe& f, const fe& g) {
   uint32_t g19[10], fa[10], fb[10];
   SV_UNROLL for (int j = 0; j < 10; ++j) g19[j] = 19u * g.v[j];
   SV_UNROLL for (int i = 0; i < 10; ++i) {
-    fa[i] = DBL ? (f.v[i] << 1) : f.v[i];
-    fb[i] = DBL ? (f.v[i] << 2) : (f.v[i] << 1);
+    fa[i] = DBL ? sv_twice(f.v[i]) : f.v[i];
+    fb[i] = sv_twice(fa[i]);  // (odd i only; unused ones are dropped)
   }
   uint64_t acc = 0, c = 0;
   SV_UNROLL for (int k = 0; k < 10; ++k) {
@@ -369,6 +382,13 @@ SV_HD void fe_sq_cm(fe& h, const fe& f) {
   fe out;
   uint64_t acc = 0, c = 0;
   int n = 0;
+  uint32_t fm[4][10];  // f << 0..3, by additions
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    fm[0][i] = f.v[i];
+    fm[1][i] = sv_twice(fm[0][i]);
+    fm[2][i] = sv_twice(fm[1][i]);
+    fm[3][i] = sv_twice(fm[2][i]);
+  }
   SV_UNROLL for (int k = 0; k < 10; ++k) {
     bool first = true;
     uint32_t A[6], B[6];
@@ -377,7 +397,7 @@ SV_HD void fe_sq_cm(fe& h, const fe& f) {
       SV_UNROLL for (int j = i; j < 10; ++j) {
         if ((i + j) % 10 != k) continue;
         const int sh = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + (DBL ? 1 : 0);
-        const uint32_t a = f.v[i] << sh;
+        const uint32_t a = fm[sh][i];
         const uint32_t b = (i + j >= 10) ? 19u * f.v[j] : f.v[j];
         A[t] = a;
         B[t] = b;
@@ -401,14 +421,30 @@ SV_HD void fe_sq_cm(fe& h, const fe& f) {
     }
 #endif
     (void)first;
+    (void)n;
     sv_col_close(out, c, acc, k);
   }
   fe_carry_wrap(out, c);
   h = out;
 }
 
+// SV_FE_ASM (device): each product / square as one generated inline-asm
+// statement (fe_asm_gen.h, tools/gen_fe_asm.py), same arithmetic as the
+// column-major forms above.
+#ifndef SV_FE_ASM
+#define SV_FE_ASM 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && SV_FE_ASM && SV_COLMAJOR && SV_MAD_ASM
+#define SV_FE_ASM_ON 1
+#include "fe_asm_gen.h"
+#else
+#define SV_FE_ASM_ON 0
+#endif
+
 SV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
-#if SV_COLMAJOR
+#if SV_FE_ASM_ON
+  fe_mul_asm(h, f, g);
+#elif SV_COLMAJOR
   fe_mul_cm<false>(h, f, g);
 #else
   uint64_t c[10];
@@ -419,7 +455,9 @@ SV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
 }
 // h = 2 f g (doubling folded into the operand; inputs must be <= R)
 SV_HD void fe_mul2(fe& h, const fe& f, const fe& g) {
-#if SV_COLMAJOR
+#if SV_FE_ASM_ON
+  fe_mul2_asm(h, f, g);
+#elif SV_COLMAJOR
   fe_mul_cm<true>(h, f, g);
 #else
   uint64_t c[10];
@@ -429,7 +467,9 @@ SV_HD void fe_mul2(fe& h, const fe& f, const fe& g) {
   SV_FENCE();
 }
 SV_HD void fe_sq(fe& h, const fe& f) {
-#if SV_COLMAJOR
+#if SV_FE_ASM_ON
+  fe_sq_asm(h, f);
+#elif SV_COLMAJOR
   fe_sq_cm<false>(h, f);
 #else
   uint64_t c[10];
@@ -440,7 +480,9 @@ SV_HD void fe_sq(fe& h, const fe& f) {
 }
 // h = 2 f^2 (input must be <= R)
 SV_HD void fe_sq2(fe& h, const fe& f) {
-#if SV_COLMAJOR
+#if SV_FE_ASM_ON
+  fe_sq2_asm(h, f);
+#elif SV_COLMAJOR
   fe_sq_cm<true>(h, f);
 #else
   uint64_t c[10];

@@ -513,7 +513,7 @@ __global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
   }
 }
 
-__global__ void sv_btab_init_kernel(uint32_t* btab) {
+__global__ __launch_bounds__(192) void sv_btab_init_kernel(uint32_t* btab) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
 #if SV_LATTICE
   // table 0: e B (also the signer's table: it reads entries <= 2^(SV_B_BITS-1));

@@ -86,6 +86,17 @@ struct Stamp {
 #define F_ADD3(i, P) "v_add3_u32 %" i ", %" i ", %16, %17\n"
 #define F_AND(i, P) "v_and_b32 %" i ", %" i ", %16\n"
 #define F_XOR(i, P) "v_xor_b32 %" i ", %" i ", %16\n"
+// VOP2 with a 32-bit literal (8-byte encoding) and with an SGPR operand
+#define F_ANDLIT(i, P) "v_and_b32 %" i ", 0x3ffffff, %" i "\n"
+#define F_ADDLIT(i, P) "v_add_u32 %" i ", 0x7ffffda, %" i "\n"
+#define F_ANDSGPR(i, P) "v_and_b32 %" i ", %17, %" i "\n"
+#define F_LSHL(i, P) "v_lshlrev_b32 %" i ", 1, %" i "\n"
+#define F_LSHLV(i, P) "v_lshlrev_b32 %" i ", %17, %" i "\n"
+#define F_ANDIC(i, P) "v_and_b32 %" i ", 7, %" i "\n"
+#define F_ADDIC(i, P) "v_add_u32 %" i ", 1, %" i "\n"
+#define F_SUB(i, P) "v_sub_u32 %" i ", %" i ", %16\n"
+#define F_CNDS(i, P) "v_cndmask_b32_e64 %" i ", %" i ", %16, %18\n"
+#define F_BFI(i, P) "v_bfi_b32 %" i ", %16, %" i ", %17\n"
 #define F_LSHLADD(i, P) "v_lshl_add_u32 %" i ", %" i ", 1, %16\n"
 #define F_ALIGNBIT(i, P) "v_alignbit_b32 %" i ", %" i ", %16, 7\n"
 #define F_BFE(i, P) "v_bfe_u32 %" i ", %" i ", 3, 25\n"
@@ -123,6 +134,18 @@ DEF_KERNEL(k_add_u32, uint32_t, F_ADD, "v"(a), "v"(b))
 DEF_KERNEL(k_add3_u32, uint32_t, F_ADD3, "v"(a), "v"(b))
 DEF_KERNEL(k_and_b32, uint32_t, F_AND, "v"(a), "v"(b))
 DEF_KERNEL(k_xor_b32, uint32_t, F_XOR, "v"(a), "v"(b))
+DEF_KERNEL(k_and_lit, uint32_t, F_ANDLIT, "v"(a), "v"(b))
+DEF_KERNEL(k_add_lit, uint32_t, F_ADDLIT, "v"(a), "v"(b))
+DEF_KERNEL(k_and_sgpr, uint32_t, F_ANDSGPR, "v"(a), "s"(__builtin_amdgcn_readfirstlane(b)))
+DEF_KERNEL(k_lshl_b32, uint32_t, F_LSHL, "v"(a), "v"(b))
+DEF_KERNEL(k_lshl_v, uint32_t, F_LSHLV, "v"(a), "v"(b & 3u))
+DEF_KERNEL(k_and_ic, uint32_t, F_ANDIC, "v"(a), "v"(b))
+DEF_KERNEL(k_add_ic, uint32_t, F_ADDIC, "v"(a), "v"(b))
+DEF_KERNEL(k_sub_u32, uint32_t, F_SUB, "v"(a), "v"(b))
+DEF_KERNEL(k_bfi_b32, uint32_t, F_BFI, "v"(a), "v"(b))
+// v_cndmask with a lane mask in an SGPR pair written by a v_cmp of this wave
+// (F_CNDMASK above reads a vcc nothing in the kernel wrote)
+DEF_KERNEL(k_cnd_sgpr, uint32_t, F_CNDS, "v"(a), "v"(b), "s"(__ballot((threadIdx.x ^ seed) & 1)))
 DEF_KERNEL(k_lshl_add_u32, uint32_t, F_LSHLADD, "v"(a), "v"(b))
 DEF_KERNEL(k_alignbit_b32, uint32_t, F_ALIGNBIT, "v"(a), "v"(b))
 DEF_KERNEL(k_bfe_u32, uint32_t, F_BFE, "v"(a), "v"(b))
@@ -130,6 +153,48 @@ DEF_KERNEL(k_cndmask_b32, uint32_t, F_CNDMASK, "v"(a), "v"(b))
 DEF_KERNEL(k_lshrrev_b64, uint64_t, F_LSHR64, "v"(a), "v"((uint64_t)b))
 DEF_KERNEL(k_lshl_add_u64, uint64_t, F_LSHLADD64, "v"(a), "v"((uint64_t)b))
 DEF_KERNEL(k_mov_dpp, uint32_t, F_MOVDPP, "v"(a), "v"(b))
+
+// Mixed streams: 8 mads interleaved with 8 other instructions on separate
+// accumulators -- are the other instructions' issue cycles additive to the
+// mads' or hidden behind them?  (lane_ops below counts both.)
+#define MIXK(NAME, OTHER)                                                                              \
+  __global__ __launch_bounds__(256) void NAME(uint32_t* out, Stamp* st, uint32_t seed) {               \
+    uint32_t a = threadIdx.x * 2654435761u + seed, b = a * 3u + 1u;                                    \
+    uint64_t m[8];                                                                                     \
+    uint32_t x[8];                                                                                     \
+    for (int i = 0; i < 8; ++i) { m[i] = a + 977u * i; x[i] = b + 13u * i; }                           \
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime(); \
+    SV_NOUNROLL_LOOP for (int it = 0; it < ITERS; ++it) {                                              \
+      asm volatile(MIX8(OTHER) MIX8(OTHER)                                                             \
+                   : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]), "+v"(m[3]), "+v"(m[4]), "+v"(m[5]), "+v"(m[6]), \
+                     "+v"(m[7]), "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), \
+                     "+v"(x[6]), "+v"(x[7])                                                            \
+                   : "v"(a), "v"(b)                                                                    \
+                   : CLOB, "vcc");                                                                     \
+    }                                                                                                  \
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime(); \
+    const unsigned w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;                                   \
+    if ((threadIdx.x & 63) == 0) st[w] = Stamp{t0, t1, r0, r1};                                        \
+    uint64_t s = 0;                                                                                    \
+    for (int i = 0; i < 8; ++i) s ^= m[i] ^ x[i];                                                      \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(s ^ (s >> 32));                            \
+  }
+// pairs (mad on m[i], OTHER on x[i]) for i = 0..7: 16 instructions
+#define MIXP(i, j, P, OTHER) "v_mad_u64_u32 %" i ", " P ", %16, %17, %" i "\n" OTHER(j)
+#define MIX8(OTHER) MIXP("0", "8", SP0, OTHER) MIXP("1", "9", SP1, OTHER) MIXP("2", "10", SP2, OTHER) \
+                    MIXP("3", "11", SP3, OTHER) MIXP("4", "12", SP4, OTHER) MIXP("5", "13", SP5, OTHER) \
+                    MIXP("6", "14", SP6, OTHER) MIXP("7", "15", SP7, OTHER)
+#define O_ADD(j) "v_add_u32 %" j ", %" j ", %16\n"
+#define O_AND(j) "v_and_b32 %" j ", 0x3ffffff, %" j "\n"
+#define O_LSHL(j) "v_lshlrev_b32 %" j ", 1, %" j "\n"
+#define O_MUL(j) "v_mul_lo_u32 %" j ", %" j ", 19\n"
+#define O_MAD(j) "v_mad_u32_u24 %" j ", %" j ", 19, %16\n"
+#define O_NOP(j) "s_nop 0\n"
+MIXK(k_mix_add, O_ADD)
+MIXK(k_mix_and, O_AND)
+MIXK(k_mix_lshl, O_LSHL)
+MIXK(k_mix_mul, O_MUL)
+MIXK(k_mix_nop, O_NOP)
 
 // float kernels (own heads: float accumulators)
 #define FKERNEL(NAME, T, F)                                                                            \
@@ -179,13 +244,28 @@ int main(int argc, char** argv) {
             {"v_addc_co_u32 (8 rotating sdst)", k_addc_co_u32, 1},
             {"v_and_b32", k_and_b32, 1},
             {"v_xor_b32", k_xor_b32, 1},
+            {"v_and_b32 32-bit literal", k_and_lit, 1},
+            {"v_add_u32 32-bit literal", k_add_lit, 1},
+            {"v_and_b32 SGPR operand", k_and_sgpr, 1},
+            {"v_lshlrev_b32 inline constant", k_lshl_b32, 1},
+            {"v_lshlrev_b32 VGPR shift", k_lshl_v, 1},
+            {"v_and_b32 inline constant", k_and_ic, 1},
+            {"v_add_u32 inline constant", k_add_ic, 1},
+            {"v_sub_u32", k_sub_u32, 1},
+            {"v_bfi_b32", k_bfi_b32, 1},
+            {"v_cndmask_b32_e64 (ballot mask in SGPRs)", k_cnd_sgpr, 1},
             {"v_lshl_add_u32", k_lshl_add_u32, 1},
             {"v_alignbit_b32", k_alignbit_b32, 1},
             {"v_bfe_u32", k_bfe_u32, 1},
             {"v_cndmask_b32", k_cndmask_b32, 1},
             {"v_lshrrev_b64", k_lshrrev_b64, 1},
             {"v_lshl_add_u64", k_lshl_add_u64, 1},
-            {"v_mov_b32_dpp quad_perm", k_mov_dpp, 1}};
+            {"v_mov_b32_dpp quad_perm", k_mov_dpp, 1},
+            {"mix: v_mad_u64_u32 + v_add_u32 (1:1)", k_mix_add, 1},
+            {"mix: v_mad_u64_u32 + v_and_b32 literal (1:1)", k_mix_and, 1},
+            {"mix: v_mad_u64_u32 + v_lshlrev_b32 (1:1)", k_mix_lshl, 1},
+            {"mix: v_mad_u64_u32 + v_mul_lo_u32 (1:1)", k_mix_mul, 1},
+            {"mix: v_mad_u64_u32 + s_nop 0 (1:1)", k_mix_nop, 1}};
   const int maxblocks = cus * 8;
   uint32_t* d_out;
   Stamp* d_st;
