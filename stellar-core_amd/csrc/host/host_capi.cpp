@@ -4,6 +4,8 @@
 // boundary.
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <future>
@@ -21,6 +23,18 @@
 using namespace stellar;
 
 namespace {
+
+// SV_HOST_TRACE: phase timings of the tx-set entry points to stderr
+const bool gPhaseTrace = getenv("SV_HOST_TRACE") != nullptr;
+struct PhaseClock {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(const char* what) {
+    if (!gPhaseTrace) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[svh] %-28s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
 thread_local std::string t_err;
 int guard_exc(std::exception const& e) {
   t_err = e.what();
@@ -150,6 +164,7 @@ void svh_set_cpu_threshold(size_t max_misses) { PubKeyUtils::setCpuBatchThreshol
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs) {
   try {
+    PhaseClock pc;
     std::vector<Hash> hashes(ntx);
     std::vector<std::vector<DecoratedSignature>> dsigs(ntx);
     std::vector<std::vector<Signer>> sgn(ntx);
@@ -158,10 +173,13 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
       dsigs[t] = sigRange(sigs, txs[t].sig_off, txs[t].nsigs);
       for (uint32_t k = 0; k < txs[t].nsigners; ++k) sgn[t].push_back(signer(signers[txs[t].signer_off + k]));
     }
+    pc.lap("txset: marshal");
     SignatureBatchPrefetch pre;
     if (use_prefetch) {
       for (size_t t = 0; t < ntx; ++t) pre.add(hashes[t], dsigs[t], sgn[t]);
+      pc.lap("txset: prefetch add");
       pre.run(use_prefetch == 2);
+      pc.lap("txset: prefetch run");
     }
     if (prefetched_pairs) *prefetched_pairs = pre.pairs();
     for (size_t t = 0; t < ntx; ++t) {
@@ -169,6 +187,7 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
       ok[t] = c.checkSignature(sgn[t], txs[t].needed_weight) ? 1 : 0;
       all_used[t] = c.checkAllSignaturesUsed() ? 1 : 0;
     }
+    pc.lap("txset: checkers");
     return SVH_OK;
   } catch (std::exception const& e) {
     return guard_exc(e);

@@ -259,9 +259,11 @@ def config3(env, n_tx=5000):
         assert rc == 0, env.host.svh_last_error_string()
         return ok, used, dt, pairs.value
 
-    ok_g, used_g, dt_g, pairs = run(1)
+    ok_g, used_g, dt_first, pairs = run(1)
+    dt_g = min([dt_first] + [run(1)[2] for _ in range(4)])  # steady state: a node checks one set per ledger
     out = {"txs": n_tx, "decorated_signatures": nsig, "prefetched_pairs": pairs, "generate_s": gen_s,
-           "gpu_prepass_checker_s": dt_g, "gpu_prepass_txs_per_s": n_tx / dt_g}
+           "gpu_prepass_checker_s": dt_g, "gpu_prepass_checker_first_call_s": dt_first,
+           "gpu_prepass_txs_per_s": n_tx / dt_g}
     if env.have_sodium:
         base = env.base
         base.cpubase_set_sodium.argtypes = [ctypes.c_char_p, ctypes.c_int]
