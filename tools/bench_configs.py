@@ -196,6 +196,32 @@ def config1(env):
     vse1 = verifysig_equivalent_rate(env, pk[:10000], sig[:10000], msgs[:10000], 32, 1)
     vsg_h, ok_h = verifysig_batch_gpu_rate(env, pk, sig, msgs, 32, keyed=False)
     vsg_k, ok_k = verifysig_batch_gpu_rate(env, pk, sig, msgs, 32, keyed=True)
+    # the engine's CPU path (host build of the same algorithm), one thread, and
+    # single verifySig calls that miss the cache (one item -> the CPU path)
+    k1 = 2000
+    t0 = time.perf_counter()
+    oc = env.sv.verify_batch_cpu(pk[:k1], sig[:k1], msgs[:k1].reshape(-1), np.arange(k1, dtype=np.uint64) * 32,
+                                 np.full(k1, 32, np.uint32), threads=1)
+    cpu_path1 = k1 / (time.perf_counter() - t0)
+    h = env.host
+    h.svh_verify_sig.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+    h.svh_cache_clear()
+    lat = []
+    single_ok = True
+    for i in range(k1):
+        a_, b_, c_ = pk[i].tobytes(), sig[i].tobytes(), msgs[i].tobytes()
+        t0 = time.perf_counter()
+        r = h.svh_verify_sig(a_, b_, 64, c_, 32)
+        lat.append(time.perf_counter() - t0)
+        single_ok = single_ok and r == 1
+    h.svh_cache_clear()
+    res["single_verifysig"] = {
+        "cpu_path_1thread_verifies_per_s": cpu_path1, "cpu_path_all_valid": bool(oc.all()),
+        "verifysig_miss_p50_us": float(np.percentile(lat, 50) * 1e6),
+        "verifysig_miss_p99_us": float(np.percentile(lat, 99) * 1e6),
+        "verifysig_all_valid": single_ok,
+        "path": "svh_verify_sig (C++ PubKeyUtils::verifySig mirror): cache miss, one item -> engine CPU path",
+    }
     res["100k_x_32B"] = {
         "gpu_verifysig_batch_host_hashed_per_s": vsg_h, "gpu_verifysig_batch_keyed_per_s": vsg_k,
         "verifysig_batch_all_valid": ok_h and ok_k,
