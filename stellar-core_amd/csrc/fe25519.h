@@ -26,6 +26,11 @@
 
 #include "sv_common.h"
 
+#if defined(SV_HOST_FE51) && !defined(__HIPCC__)
+// host CPU path: radix 2^51 (fe51_host.h), same interface and bound contract
+#include "fe51_host.h"
+#else
+
 struct fe {
   uint32_t v[10];
 };
@@ -613,3 +618,5 @@ SV_HD void fe_const_sqrtm1(fe& h) {
                           0x1fbd7a7, 0x2804c9e, 0x1e16569, 0x004fc1d, 0x0ae0c92};
   SV_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = c[i];
 }
+
+#endif  // SV_HOST_FE51

@@ -4,9 +4,11 @@
 // libsodium's crypto_sign_verify_detached, SHA-512(R || A || M) mod L, the
 // half-size equation [c1 S mod L] B + [c0](-A) + [c1](-R) == O of lattice.h --
 // compiled from the same headers for the host (g++: SV_HD = static inline).
-// Only the base-point digit radix differs: 2^8 instead of 2^16, so the two
-// host tables (e B and e 2^128 B, e <= 128) are 2 x 129 entries built in a few
-// milliseconds at first use instead of the GPU's 2 x 32769.
+// Two things differ: the base-point digit radix is 2^8 instead of 2^16, so the
+// two host tables (e B and e 2^128 B, e <= 128) are 2 x 129 entries built in a
+// few milliseconds at first use instead of the GPU's 2 x 32769; and the field
+// elements are 5 x 51-bit limbs (fe51_host.h) instead of the device's 10 x
+// 25.5-bit ones, behind the same interface.
 //
 // Role: an engine error is never a reject -- the
 // caller re-runs the batch here -- and a single verifySig is cheaper here than
@@ -15,6 +17,10 @@
 // (/root/reference/src/crypto/SecretKey.cpp:461-463).  Not the oracle: nothing
 // under oracle/ is compiled or linked here.
 #define SV_LB_BITS 8
+// field arithmetic in radix 2^51 with 128-bit products (fe51_host.h): what
+// x86-64 multiplies fastest; the device form's 10 x 32-bit limbs would cost 4x
+// the multiplications here
+#define SV_HOST_FE51 1
 #include "verify_core.h"
 
 #include <algorithm>
