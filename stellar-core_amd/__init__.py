@@ -25,8 +25,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libstellar_sigverify.so")
 
 
-VERIFY_KERNEL_SOURCES = ("sv_common.h", "fe25519.h", "ge25519.h", "sc25519.h", "lattice.h", "sha512_dev.h", "verify_core.h",
-                         "quad.h", "sv_kernels.hip")
+VERIFY_KERNEL_SOURCES = ("sv_common.h", "fe25519.h", "fe_asm_gen.h", "ge25519.h", "sc25519.h", "lattice.h", "sha512_dev.h",
+                         "verify_core.h", "quad.h", "sv_kernels.hip")
 
 # kernel paths (include/stellar_sigverify.h)
 PATH_AUTO, PATH_THROUGHPUT, PATH_LATENCY = 0, 1, 2
