@@ -357,6 +357,19 @@ Scratch& scratch() {
   return s;
 }
 
+// Fills in this batch's pending values: item k's entry is ids[k] (kNone: no
+// pending insert), under the cache mutex.  (Split over 4 helper threads by
+// entry id it measured slower than this prefetching loop: 0.40 vs 0.29 ms per
+// 100k on MI355X hosts.)
+void resolvePending(const uint32_t* ids, const uint8_t* v, size_t n, uint64_t owner) {
+  constexpr uint32_t kNone = RandomEvictionCache::kNone;
+  std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
+  for (size_t k = 0; k < n; ++k) {
+    if (k + 8 < n && ids[k + 8] != kNone) gVerifySigCache.prefetchEntry(ids[k + 8]);
+    if (ids[k] != kNone) gVerifySigCache.resolve(ids[k], owner, (uint32_t)k, v[k] != 0);
+  }
+}
+
 void packForTestHook(std::vector<Item> const& items, std::vector<size_t> const& rows, Scratch& st) {
   const size_t n = rows.size();
   st.ppk.resize(32 * n);
@@ -543,13 +556,11 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
       cpuVerify(items, rows, verdict.data());
     }
     if (!walked) phase1();  // (not reached: the engine ran it on success)
-    {
-      std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
-      for (size_t e = 0; e < E; ++e) {
-        if (e + 8 < E && pid[e + 8] != kNone) gVerifySigCache.prefetchEntry(pid[e + 8]);
-        if (pid[e] != kNone) gVerifySigCache.resolve(pid[e], owner, (uint32_t)e, verdict[e] != 0);
-      }
-    }
+    const auto tE = std::chrono::steady_clock::now();
+    resolvePending(pid.data(), verdict.data(), E, owner);
+    if (trace)
+      fprintf(stderr, "[verifySigBatch keyed n=%zu] resolve %.3f ms\n", E,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tE).count());
     for (size_t e = 0; e < E; ++e)
       if (!hit[e]) out[rows[e]] = verdict[e] != 0;
   } else {
@@ -607,10 +618,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
       }
     }
     // phase 3: fill in the pending values
-    {
-      std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
-      for (size_t m = 0; m < M; ++m) gVerifySigCache.resolve(missIds[m], owner, (uint32_t)m, mv[m] != 0);
-    }
+    resolvePending(missIds.data(), mv.data(), M, owner);
     for (size_t e = 0; e < E; ++e)
       if (ref[e] != RandomEvictionCache::kNone) out[rows[e]] = mv[ref[e]] != 0;
   }
