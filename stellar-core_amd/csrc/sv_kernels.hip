@@ -434,6 +434,7 @@ __global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
   sv_unpack2(R, p.sig + 4 * ii);
   bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
             sv_point_canonical(R);
+#ifndef SV_QPROF_NODEC  // (developer A/B builds only: phase timing of this kernel)
   {
     // decompress: even roles -A, odd roles -R; roles 0 / 1 keep their table
     uint32_t E[8];
@@ -457,13 +458,18 @@ __global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
       if (store) sv_store_lentry((sv_u4*)(tab + e * SV_QENT_DW), ce);
     }
   }
+#endif
   sv_lat lat;
   {
     uint32_t h[8];
     sc_reduce512(h, hram);
     sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
   }
+#ifdef SV_QPROF_NOMUL
+  const int W = 0;
+#else
   const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
+#endif
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
   __syncthreads();  // tables visible to the whole quad
