@@ -398,6 +398,9 @@ __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cpa
 // multiplication runs with every point operation split over the quad.
 // Verdict bytes by role-0 lanes; the bitmap as one 16-bit store per workgroup
 // (bits 16 k .. 16 k + 15 of word k / 4).
+#ifndef SV_LAT_OCTET
+#define SV_LAT_OCTET 1
+#endif
 #define SV_QSIGS 16
 #define SV_QENT_DW 40  // cached entry: YpX, YmX, Z, T2d x 10 dwords
 
@@ -516,6 +519,132 @@ __global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
     uint16_t m16 = 0;
     SV_UNROLL for (int k = 0; k < SV_QSIGS; ++k) m16 |= (uint16_t)(((bal >> (4 * k)) & 1u) << k);
     ((uint16_t*)p.bitmap)[blockIdx.x] = m16;
+  }
+}
+
+// ------------------------------------------- latency path, two quads per signature
+// (SV_LAT_OCTET, default) One signature per OCTET of lanes: the two quads of
+// the octet evaluate the two halves of (*) in lattice.h in parallel,
+//   quad 0:  P_A = [c0](-A) + [s_lo] B           (table_A, e B)
+//   quad 1:  P_R = [c1](-R) + [s_hi] 2^128 B     (table_R, e 2^128 B)
+// over the same W windows (each quad: 4 doublings, ONE table addition and, on
+// base windows, ONE base-point addition per window, every point operation
+// split over its 4 lanes as in quad.h), then quad 0 adds P_R (fetched from
+// lanes + 4 by DPP row_shl:4) and tests P_A + P_R for the identity.  Against
+// one quad per signature this removes one variable and one base addition per
+// window from the serial chain; quad 0 decompresses A and quad 1 R, as the
+// even / odd lanes of a quad did before.  8 signatures per single-wave
+// workgroup.
+#define SV_OSIGS 8
+
+// value of lane + 4 (row_shl:4 within each row of 16: lanes 0-3 <- 4-7 and
+// 8-11 <- 12-15, i.e. quad 0 of every octet reads quad 1)
+__device__ __forceinline__ uint32_t oc_from_hi(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xf, 0xf, false);
+}
+__device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
+  SV_UNROLL for (int i = 0; i < 10; ++i) o.v[i] = oc_from_hi(f.v[i]);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64, 1) void sv_octet_kernel(sv_kparams p) {
+  __shared__ uint32_t s_tab[SV_OSIGS][2][SV_ATAB_ENTRIES][SV_QENT_DW];  // 23 KB
+  const uint32_t lane = threadIdx.x;
+  const uint32_t role = lane & 3u, half = (lane >> 2) & 1u, sl = lane >> 3;
+  const qd_role q{role == 1, role == 2, role == 3};
+  const uint64_t i = (uint64_t)blockIdx.x * SV_OSIGS + sl;
+  const bool active = i < p.n;
+  const uint64_t ii = active ? i : p.n - 1;  // idle tail octets redo the last item
+  uint32_t A[8], S[8], hram[16], R[8];
+  sv_load_and_hash<MODE>(p, ii, A, S, hram);
+  sv_unpack2(R, p.sig + 4 * ii);
+  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
+            sv_point_canonical(R);
+  {
+    // decompress: quad 0 -A, quad 1 -R; role 0 of each quad stores its table
+    uint32_t E[8];
+    SV_UNROLL for (int k = 0; k < 8; ++k) E[k] = half ? R[k] : A[k];
+    ge_p3 Pt;
+    const uint32_t dok = ge_frombytes(Pt, E, true) ? 1u : 0u;
+    ok = ok && (dok & oc_from_hi(dok)) != 0;  // (valid on quad 0, the lanes that use it)
+    ge_cached c1, ce;
+    ge_p3_to_cached(c1, Pt);
+    ge_cached_identity(ce);
+    uint32_t* tab = &s_tab[sl][half][0][0];
+    const bool store = role == 0;
+    if (store) sv_store_lentry((sv_u4*)tab, ce);
+    if (store) sv_store_lentry((sv_u4*)(tab + SV_QENT_DW), c1);
+    ge_p3 P3 = Pt;
+    ge_p1p1 Qa;
+    SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
+      ge_add_preswapped(Qa, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, false);
+      ge_p1p1_to_p3(P3, Qa);
+      ge_p3_to_cached(ce, P3);
+      if (store) sv_store_lentry((sv_u4*)(tab + e * SV_QENT_DW), ce);
+    }
+  }
+  sv_lat lat;
+  {
+    uint32_t h[8];
+    sc_reduce512(h, hram);
+    sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
+  }
+  const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
+  sv_lat_digits D;
+  sv_lat_prepare(D, lat, S, W);
+  __syncthreads();  // tables visible to the whole quad
+
+  const sv_u4* btab = p.btab + (half ? SV_LBTAB_ENTRIES * SV_BTAB_QUADS : 0);
+  const uint32_t* tab = &s_tab[sl][half][0][0];
+  // this quad's digit string and its top-digit carry
+  uint32_t dg[8];
+  SV_UNROLL for (int k = 0; k < 8; ++k) dg[k] = half ? D.dR[k] : D.dA[k];
+  const bool top8 = half ? D.top8R : D.top8A;
+  const bool flip = half && D.rneg;
+  ge_p3 P;
+  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
+  SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
+    int32_t d = sc_pop_top(dg, 4);
+    if (w == W - 1 && top8) d = 8;
+    if (flip) d = -d;
+    int32_t dB0, dB1;
+    fe b;
+    const bool bwin = sv_lat_bdigits(D, w, dB0, dB1);
+    const int32_t dB = half ? dB1 : dB0;
+    if (bwin) qd_load_affine(b, btab + (dB < 0 ? -dB : dB) * SV_BTAB_QUADS, role, dB < 0);  // lands during the doublings
+    if (w != W - 1) {
+      SV_NOUNROLL for (int k = 0; k < 4; ++k) qd_dbl(P, q, k == 3);
+    }
+    fe m;
+    qd_load_cached(m, tab + (d < 0 ? -d : d) * SV_QENT_DW, role, d < 0);
+    // T is needed after this addition by a base addition or, after the last
+    // window, by the final combination
+    qd_add(P, m, q, d < 0, bwin || w == 0);
+    if (bwin) qd_add(P, b, q, dB < 0, w == 0);
+  }
+  // quad 0: P_A + P_R, P_R in cached form from quad 1
+  {
+    ge_p3 PR;
+    fe_from_hi(PR.X, P.X);
+    fe_from_hi(PR.Y, P.Y);
+    fe_from_hi(PR.Z, P.Z);
+    fe_from_hi(PR.T, P.T);
+    fe d2, t2d, ypx, ymx, mine;
+    fe_const_2d(d2);
+    fe_mul(t2d, PR.T, d2);
+    fe_add(ypx, PR.Y, PR.X);
+    fe_sub(ymx, PR.Y, PR.X);
+    fe_pick4(mine, q, t2d, PR.Z, ypx, ymx);  // role 0 2dT, 1 Z, 2 Y+X, 3 Y-X (qd_add's operand order)
+    qd_add(P, mine, q, false, false);
+  }
+  ok = ok && sv_is_identity(P);
+  const bool owner = half == 0 && role == 0;
+  if (active && owner) p.verdict[i] = ok ? 1 : 0;
+  const uint64_t bal = __ballot(ok && active && owner);
+  if (p.bitmap != nullptr && lane == 0) {
+    uint8_t m8 = 0;
+    SV_UNROLL for (int k = 0; k < SV_OSIGS; ++k) m8 |= (uint8_t)(((bal >> (8 * k)) & 1u) << k);
+    ((uint8_t*)p.bitmap)[blockIdx.x] = m8;
   }
 }
 
@@ -678,6 +807,15 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
   p.dbg = dbg;
 #if SV_LATTICE
   if (path == 2) {  // SV_PATH_LATENCY
+#if SV_LAT_OCTET
+    const unsigned og = (unsigned)((n + SV_OSIGS - 1) / SV_OSIGS);
+    if (mode == 0)
+      hipLaunchKernelGGL(sv_octet_kernel<0>, dim3(og), dim3(64), 0, s, p);
+    else if (mode == 1)
+      hipLaunchKernelGGL(sv_octet_kernel<1>, dim3(og), dim3(64), 0, s, p);
+    else
+      hipLaunchKernelGGL(sv_octet_kernel<2>, dim3(og), dim3(64), 0, s, p);
+#else
     const unsigned qg = (unsigned)((n + SV_QSIGS - 1) / SV_QSIGS);
     if (mode == 0)
       hipLaunchKernelGGL(sv_quick_kernel<0>, dim3(qg), dim3(64), 0, s, p);
@@ -685,6 +823,7 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
       hipLaunchKernelGGL(sv_quick_kernel<1>, dim3(qg), dim3(64), 0, s, p);
     else
       hipLaunchKernelGGL(sv_quick_kernel<2>, dim3(qg), dim3(64), 0, s, p);
+#endif
     return hipGetLastError();
   }
 #endif
