@@ -574,11 +574,14 @@ __global__ __launch_bounds__(64, 1) void sv_octet_kernel(sv_kparams p) {
     const bool store = role == 0;
     if (store) sv_store_lentry((sv_u4*)tab, ce);
     if (store) sv_store_lentry((sv_u4*)(tab + SV_QENT_DW), c1);
+    // entries 2..8 by repeated addition of P, each addition split over the
+    // quad (qd_add: one product per lane and stage) instead of one lane's
+    // serial 8 products
+    fe mine;
+    fe_pick4(mine, q, c1.T2d, c1.Z, c1.YpX, c1.YmX);
     ge_p3 P3 = Pt;
-    ge_p1p1 Qa;
     SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
-      ge_add_preswapped(Qa, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, false);
-      ge_p1p1_to_p3(P3, Qa);
+      qd_add(P3, mine, q, false, true);
       ge_p3_to_cached(ce, P3);
       if (store) sv_store_lentry((sv_u4*)(tab + e * SV_QENT_DW), ce);
     }
