@@ -23,8 +23,12 @@
 #define SV_STAGE_A 1  // table_A entries via LDS-DMA prefetch (verify_core.h)
 #endif
 #define SV_WAVES_PER_SIMD 2
+// sv_main_kernel runs at 3 waves/SIMD (168 VGPRs): with its digits streamed
+// from the record and one base address per staged entry it fits without
+// spills in the loop; measured 1-1.5 % faster than 2 waves
+// (profiles/r02/ab_main_waves.txt)
 #ifndef SV_MAIN_WAVES
-#define SV_MAIN_WAVES SV_WAVES_PER_SIMD
+#define SV_MAIN_WAVES 3
 #endif
 // 1: verify through the half-size equation (lattice.h, ~130 doublings per
 // signature); 0: the direct 253-bit ladder (sv_verify_kernel below).
@@ -343,6 +347,91 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   SV_PHASE(4);
 }
 
+// The main kernel's scalar multiplication: the step machine of
+// sv_lat_scalarmult (verify_core.h, STAGED with one stage region) with the
+// digits streamed from the signature's record instead of held in registers
+// (33 VGPRs -> 7: what lets the kernel run at 3 waves/SIMD without spills).
+// Record words (sv_prep_kernel): dA[0..7], dR[8..15] = the radix-16 digit
+// strings after sv_lat_prepare's shift, so window w's digit is nibble
+// p = w + 64 - W; dB0[16..23], dB1[24..31] = base-point digits j (window 4j).
+__device__ __forceinline__ int32_t sv_nibble(uint32_t word, int p) {
+  return (int32_t)__builtin_amdgcn_sbfe((int)word, (unsigned)(4 * (p & 7)), 4u);
+}
+__device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw, uint32_t flags, int W,
+                                                   const sv_u4* tabA, const sv_u4* tabR, const sv_u4* btab0,
+                                                   const sv_u4* btab1, sv_u4* stage) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const bool top8A = (flags & SV_REC_TOP8A) != 0, top8R = (flags & SV_REC_TOP8R) != 0;
+  const bool rneg = (flags & SV_REC_RNEG) != 0;
+  // current and next digit words (the word changes every 8 windows)
+  uint32_t curA = rw[7], curR = rw[15], nxtA = rw[6], nxtR = rw[14];
+  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
+  ge_p1p1 Q;
+  SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
+    const int pos = w + 64 - W;  // (wave-uniform)
+    if ((pos & 7) == 7 && w != W - 1) {
+      curA = nxtA;
+      curR = nxtR;
+      const int k = (pos >> 3) - 1;
+      if (k >= 0) {
+        nxtA = rw[k];
+        nxtR = rw[8 + k];
+      }
+    }
+    int32_t dA = sv_nibble(curA, pos), dR = sv_nibble(curR, pos);
+    if (w == W - 1) {
+      if (top8A) dA = 8;
+      if (top8R) dR = 8;
+    }
+    if (rneg) dR = -dR;
+    const bool bwin = w % SV_LB_WIN == 0 && w / SV_LB_WIN < SV_LB_DIGITS;
+    int32_t dB0 = 0, dB1 = 0;
+    if (bwin) {
+      dB0 = (int32_t)rw[16 + w / SV_LB_WIN];
+      dB1 = (int32_t)rw[16 + SV_LB_DIGITS + w / SV_LB_WIN];
+    }
+    const int nsteps = bwin ? 8 : 6;
+    const int s0 = (w == W - 1) ? 4 : 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sv_stage_lentry(stage, tabA + (dA < 0 ? -dA : dA) * SV_LTAB_QUADS);
+    SV_NOUNROLL for (int s = s0; s < nsteps; ++s) {
+      if (s < 4) {
+        ge_dbl(Q, P.X, P.Y, P.Z);
+      } else {
+        fe qa, qb, qz, qt;
+        bool neg;
+        const bool zone = s >= 6;
+        // the entry DMA'd for this step (and any digit load) has landed; once
+        // the entry is read, the stage receives the next addition's entry
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!zone) {
+          neg = (s == 4 ? dA : dR) < 0;
+          sv_load_lentry(qa, qb, qz, qt, stage + __lane_id(), 64, neg);
+          if (s == 4 || bwin) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (s == 4) sv_stage_lentry(stage, tabR + (dR < 0 ? -dR : dR) * SV_LTAB_QUADS);
+            else sv_stage_bentry(stage, btab0, dB0);
+          }
+        } else {
+          neg = (s == 6 ? dB0 : dB1) < 0;
+          fe_1(qz);
+          const sv_u4* st = stage + __lane_id();
+          sv_load_fe3(qa, st, 64);
+          sv_load_fe3(qb, st + 3 * 64, 64);
+          sv_load_fe3(qt, st + 6 * 64, 64);
+          if (s == 6) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            sv_stage_bentry(stage, btab1, dB1);
+          }
+        }
+        ge_add_preswapped(Q, P, qa, qb, qz, qt, neg, zone);
+      }
+      ge_p1p1_to_p3_opt(P, Q, s + 1 >= 4 && s + 1 < nsteps);
+    }
+  }
+#endif
+}
+
 __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cparams c) {
   const sv_kparams& p = c.k;
   __shared__ sv_u4 s_stage[SV_BLOCK / 64][(SV_STAGE_ONE ? 1 : 2) * SV_LTAB_QUADS * 64];  // per-wave entry stage
@@ -357,32 +446,12 @@ __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cpa
     const bool active = li < c.cnt;
     const sv_u4* tabA = p.ws + li * SV_SLOT_QUADS_L;
     const sv_u4* tabR = tabA + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
-    const sv_u4* r = c.rec + li * SV_REC_QUADS;
-    sv_lat_digits D;
-    bool pre_ok;
-    {
-      uint32_t rw[4 * SV_REC_QUADS];
-      SV_UNROLL for (int k = 0; k < SV_REC_QUADS; ++k) {
-        const sv_u4 q = r[k];
-        rw[4 * k] = q.x; rw[4 * k + 1] = q.y; rw[4 * k + 2] = q.z; rw[4 * k + 3] = q.w;
-      }
-      SV_UNROLL for (int k = 0; k < 8; ++k) {
-        D.dA[k] = rw[k];
-        D.dR[k] = rw[8 + k];
-      }
-      SV_UNROLL for (int k = 0; k < SV_LB_DIGITS; ++k) {
-        D.dB0[k] = (int32_t)rw[16 + k];
-        D.dB1[k] = (int32_t)rw[16 + SV_LB_DIGITS + k];
-      }
-      const uint32_t flags = rw[16 + 2 * SV_LB_DIGITS];
-      D.rneg = (flags & SV_REC_RNEG) != 0;
-      D.top8A = (flags & SV_REC_TOP8A) != 0;
-      D.top8R = (flags & SV_REC_TOP8R) != 0;
-      pre_ok = (flags & SV_REC_OK) != 0;
-    }
+    const uint32_t* rw = (const uint32_t*)(c.rec + li * SV_REC_QUADS);
+    const uint32_t flags = rw[16 + 2 * SV_LB_DIGITS];
+    const bool pre_ok = (flags & SV_REC_OK) != 0;
     const int W = (int)__builtin_amdgcn_readfirstlane(c.wmax[li >> 6]);
     ge_p3 P;
-    sv_lat_scalarmult<true>(P, D, W, tabA, tabR, btab0, btab1, stage);
+    sv_main_scalarmult(P, rw, flags, W, tabA, tabR, btab0, btab1, stage);
     const bool ok = pre_ok && sv_is_identity(P) && active;
     if (active) p.verdict[c.start + li] = ok ? 1 : 0;
     const uint64_t mask = __ballot(ok);

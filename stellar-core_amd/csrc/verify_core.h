@@ -158,6 +158,17 @@ SV_COLD void sv_build_atab(sv_u4* slot, int qstride, const ge_p3& negA) {
 #define SV_STAGE_QUADS ((SV_ATAB_QUADS + (SV_STAGE_B ? SV_BTAB_QUADS : 0)) * 64)
 
 #if defined(__HIP_DEVICE_COMPILE__)
+// LDS-DMA of quad Q of an entry at per-lane address SRC + 16*OFF bytes into
+// stage row ROW (lane-linear, 1 KiB per row).  The instruction's immediate
+// offset is added to BOTH the global and the LDS address (tools/glds_off.hip,
+// measured on MI355X), so the LDS pointer handed over is pre-biased by it:
+// one per-lane base address serves all quads of an entry.  (With a pointer
+// per quad the compiler hoisted ~30 64-bit addresses per window and kept them
+// live: ~60 VGPRs, spilled at 3 waves/SIMD.)
+#define SV_GLDS(SRC, OFF, STAGE, ROW)                                                                 \
+  __builtin_amdgcn_global_load_lds(                                                                   \
+      (const void*)(SRC),                                                                             \
+      (__attribute__((address_space(3))) void*)((char*)((STAGE) + (ROW) * 64) - 16 * (OFF)), 16, 16 * (OFF), 0)
 // Device: the window's table_A entry is fetched by LDS-DMA (global_load_lds,
 // no VGPR destination) when the window starts, so the HBM/L2 latency hides
 // behind the window's 4 doublings instead of stalling the addition.  The
@@ -183,11 +194,11 @@ SV_HD void sv_stage_bentry(sv_u4* stageB, const sv_u4* btab, int32_t d) {
   const sv_u4* e = btab + (neg ? -d : d) * SV_BTAB_QUADS;
   const sv_u4* ea = e + (neg ? 3 : 0);
   const sv_u4* eb = e + (neg ? 0 : 3);
-  SV_UNROLL for (int q = 0; q < SV_BTAB_QUADS; ++q) {
-    const sv_u4* src = q < 3 ? ea + q : (q < 6 ? eb + (q - 3) : e + q);
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(stageB + q * 64),
-                                     16, 0, 0);
-  }
+  // rows 0-2 from ea, 3-5 from eb, 6-8 from e + 6.. (three base addresses)
+  SV_GLDS(ea, 0, stageB, 0); SV_GLDS(ea, 1, stageB, 1); SV_GLDS(ea, 2, stageB, 2);
+  SV_GLDS(eb, 0, stageB, 3); SV_GLDS(eb, 1, stageB, 4); SV_GLDS(eb, 2, stageB, 5);
+  SV_GLDS(e, 6, stageB, 6); SV_GLDS(e, 7, stageB, 7); SV_GLDS(e, 8, stageB, 8);
+  static_assert(SV_BTAB_QUADS == 9, "entry size");
 }
 // hipcc does not count LDS-DMA completion before LDS reads: wait explicitly
 // (no other vector-memory op is in flight inside the window).
@@ -649,11 +660,13 @@ SV_COLD void sv_lat_prepare(sv_lat_digits& D, const sv_lat& lat, const uint32_t 
 #define SV_LAT_STAGE_B 1
 #endif
 #if defined(__HIP_DEVICE_COMPILE__)
-// LDS-DMA of one lane-contiguous 10-quad table entry into a lane-linear stage
+// one lane-contiguous 10-quad table entry into a lane-linear stage
 SV_HD void sv_stage_lentry(sv_u4* stage, const sv_u4* entry) {
-  SV_UNROLL for (int q = 0; q < SV_LTAB_QUADS; ++q)
-    __builtin_amdgcn_global_load_lds((const void*)(entry + q), (__attribute__((address_space(3))) void*)(stage + q * 64),
-                                     16, 0, 0);
+  SV_GLDS(entry, 0, stage, 0); SV_GLDS(entry, 1, stage, 1); SV_GLDS(entry, 2, stage, 2);
+  SV_GLDS(entry, 3, stage, 3); SV_GLDS(entry, 4, stage, 4); SV_GLDS(entry, 5, stage, 5);
+  SV_GLDS(entry, 6, stage, 6); SV_GLDS(entry, 7, stage, 7); SV_GLDS(entry, 8, stage, 8);
+  SV_GLDS(entry, 9, stage, 9);
+  static_assert(SV_LTAB_QUADS == 10, "entry size");
 }
 #endif
 
