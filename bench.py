@@ -113,6 +113,83 @@ def sodium_path():
     return None
 
 
+def verifysig_equivalent_rate(sv, spath, pk, sig, msg, mlen, threads):
+    """The reference's PubKeyUtils::verifySig on `threads` threads: the C++
+    mirror (BLAKE2b cache key, 0xffff-entry cache behind its mutex) with one
+    libsodium call per miss behind it (SecretKey.cpp:435-468), cache cleared
+    first.  Native harness oracle/cpu_baseline.c cpubase_verifysig_threads."""
+    base = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+    host = ctypes.CDLL(sv.HOSTLIB_PATH)
+    base.cpubase_set_sodium.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    if base.cpubase_set_sodium(spath.encode(), 1) != 0:
+        raise RuntimeError("libsodium setup failed")
+    base.cpubase_verifysig_threads.restype = ctypes.c_double
+    base.cpubase_verifysig_threads.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    host.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+    n = pk.shape[0]
+    pk, sig, msg = (np.ascontiguousarray(x) for x in (pk, sig, msg))
+    off = np.arange(n, dtype=np.uint64) * mlen
+    ln = np.full(n, mlen, np.uint32)
+    out = np.zeros(n, np.uint8)
+    host.svh_set_test_verifier(ctypes.cast(base.cpubase_sodium_batch, ctypes.c_void_p))
+    host.svh_cache_clear()
+    try:
+        dt = base.cpubase_verifysig_threads(ctypes.cast(host.svh_verify_sig, ctypes.c_void_p), pk.ctypes.data,
+                                            sig.ctypes.data, msg.ctypes.data, off.ctypes.data, ln.ctypes.data, n,
+                                            threads, out.ctypes.data)
+    finally:
+        host.svh_set_test_verifier(None)
+        host.svh_cache_clear()
+    if dt <= 0:
+        raise RuntimeError("verifySig harness failed (%s)" % dt)
+    return n / dt, out
+
+
+def config1(sv, sodium, spath, pk_h, sig_h, msgs, threads, device):
+    """BASELINE config 1 / SURVEY.md §8 d2, both shapes: 100k x 32-byte hashes
+    (BASELINE.json; the bench dataset's first 100k) and the reference's own
+    benchmark shape, 10k keypairs x 256-byte messages (SecretKey.cpp:182-234,
+    CryptoTests.cpp:299-306; libsodium-signed here).  Raw libsodium and the
+    verifySig equivalent, 1 thread and all cores, beside the GPU host API."""
+    out = {}
+    k = min(100_000, pk_h.shape[0])
+    shapes = [("100k_x_32B", pk_h[:k], sig_h[:k], msgs[:32 * k].reshape(k, 32), 32, 16384)]
+    pks, sgs, ms = [], [], []
+    for i in range(10_000):
+        m = hashlib.shake_256(b"REF256" + struct.pack("<Q", i)).digest(256)
+        pkb = ctypes.create_string_buffer(32)
+        skb = ctypes.create_string_buffer(64)
+        sodium.crypto_sign_seed_keypair(pkb, skb, hashlib.sha256(b"REFKEY" + struct.pack("<Q", i)).digest())
+        sb = ctypes.create_string_buffer(64)
+        sodium.crypto_sign_detached(sb, None, m, ctypes.c_ulonglong(256), skb)
+        pks.append(pkb.raw); sgs.append(sb.raw); ms.append(m)
+    shapes.append(("ref_shape_10k_x_256B", np.frombuffer(b"".join(pks), np.uint8).reshape(-1, 32),
+                   np.frombuffer(b"".join(sgs), np.uint8).reshape(-1, 64),
+                   np.frombuffer(b"".join(ms), np.uint8).reshape(-1, 256), 256, 10_000))
+    for name, pk, sg, m, mlen, st in shapes:
+        sv.verify_fixed(pk[:1024], sg[:1024], m[:1024], mlen, device=device)
+        best, g_ok = None, True
+        for _ in range(3):
+            t1 = time.perf_counter()
+            o = sv.verify_fixed(pk, sg, m, mlen, device=device)
+            dt = time.perf_counter() - t1
+            g_ok = g_ok and bool(o.all())
+            best = dt if best is None else min(best, dt)
+        c_t, _, o1 = cpu_verify_rate(pk, sg, m.reshape(-1), mlen, threads, spath)
+        c_1, _, o2 = cpu_verify_rate(pk[:st], sg[:st], m[:st].reshape(-1), mlen, 1, spath)
+        v_1, o3 = verifysig_equivalent_rate(sv, spath, pk[:st], sg[:st], m[:st], mlen, 1)
+        v_t, o4 = verifysig_equivalent_rate(sv, spath, pk, sg, m, mlen, threads)
+        out[name] = {
+            "signatures": int(pk.shape[0]), "msg_len": mlen,
+            "gpu_host_api_verifies_per_s": pk.shape[0] / best,
+            "cpu_libsodium_threads": c_t, "cpu_libsodium_1thread": c_1,
+            "cpu_verifysig_equivalent_threads": v_t, "cpu_verifysig_equivalent_1thread": v_1,
+            "cpu_threads": threads, "single_thread_sample": st,
+            "all_valid": bool(g_ok and o1.all() and o2.all() and o3.all() and o4.all()),
+        }
+    return out
+
+
 def scp_latency_set(sodium, n=1000, adversarial=0.1, seed=20250211):
     """Config 4: 100 validators, 1000 signatures over 128-384 B messages, 10% adversarial."""
     rng = np.random.default_rng(seed)
@@ -162,6 +239,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-host-api", action="store_true")
+    ap.add_argument("--no-config1", action="store_true", help="skip the config-1 CPU/host-API block")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -414,6 +492,10 @@ def main():
             "cpu_verdicts_all_valid": bool(out.all() and out1.all()),
             "gpu_over_cpu": value / rate if rate > 0 else None,
         }
+        if spath is not None and not args.no_config1:
+            t_c1 = time.perf_counter()
+            result["config1"] = config1(sv, sodium, spath, pk_h, sig_h, msgs, threads, local)
+            log("config 1 (both shapes) in %.1fs" % (time.perf_counter() - t_c1))
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -212,10 +212,14 @@ int sv_sha256_device(int device, const void* d_data, const uint64_t* d_off, cons
  * fallback pair (h, 1) of the half-size equation (lattice.h), i.e. the
  * full-length scalar; MAX_WINDOWS: every wave runs all 64 windows; FAIL: every
  * GPU entry point returns SV_ERR_HIP without touching the device (callers'
- * CPU fallback tests).  Returns the previous flags, or SV_ERR_INVALID_ARG. */
+ * CPU fallback tests); PREP_ONLY (profiling): throughput-path launches run the
+ * per-signature prep kernel only (verdicts are NOT written), so kernel-time
+ * accounting splits into prep and scalar multiplication.  Returns the previous
+ * flags, or SV_ERR_INVALID_ARG. */
 #define SV_DBG_TRIVIAL_PAIR 0x1u
 #define SV_DBG_MAX_WINDOWS 0x2u
 #define SV_DBG_FAIL 0x4u
+#define SV_DBG_PREP_ONLY 0x8u
 int sv_set_debug_flags(uint32_t flags);
 
 /* Bytes of the slot's kernel workspace / pinned staging currently allocated. */

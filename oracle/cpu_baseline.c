@@ -105,6 +105,11 @@ int cpubase_sodium_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   if (!g_sodium_fn) return -1;
   int T = g_threads;
   if ((size_t)T > n) T = n ? (int)n : 1;
+  if (T == 1) {  /* inline: a per-call thread would dominate single-signature calls */
+    struct vjob j = {pk, sig, msg, off, len, 0, n, verdict};
+    vworker(&j);
+    return 0;
+  }
   pthread_t th[256];
   struct vjob jobs[256];
   for (int t = 0; t < T; ++t) {
@@ -116,4 +121,46 @@ int cpubase_sodium_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   }
   for (int t = 0; t < T; ++t) pthread_join(th[t], 0);
   return 0;
+}
+
+/* The reference's verifySig on every core: `threads` pthreads, each calling
+ * `verify_sig` (the C++ PubKeyUtils::verifySig mirror, svh_verify_sig:
+ * BLAKE2b cache key, global cache under its mutex, then the batch verifier --
+ * set to cpubase_sodium_batch with one thread, i.e. one libsodium call per
+ * miss, as SecretKey.cpp:435-468 does) for its contiguous slice.  Returns
+ * wall seconds (< 0 on error). */
+typedef int (*verifysig_fn)(const uint8_t*, const uint8_t*, size_t, const uint8_t*, size_t);
+struct sjob {
+  verifysig_fn f;
+  const uint8_t *pk, *sig, *msg;
+  const uint64_t* off;
+  const uint32_t* len;
+  size_t lo, hi;
+  uint8_t* out;
+};
+
+static void* sworker(void* arg) {
+  struct sjob* j = (struct sjob*)arg;
+  for (size_t i = j->lo; i < j->hi; ++i)
+    j->out[i] = j->f(j->pk + 32 * i, j->sig + 64 * i, 64, j->msg + j->off[i], j->len[i]) == 1;
+  return 0;
+}
+
+double cpubase_verifysig_threads(verifysig_fn f, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                                 const uint64_t* off, const uint32_t* len, size_t n, int threads, uint8_t* out) {
+  if (!f) return -2.0;
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  struct sjob jobs[256];
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < threads; ++t) {
+    struct sjob j = {f, pk, sig, msg, off, len, (size_t)t * n / threads, (size_t)(t + 1) * n / threads, out};
+    jobs[t] = j;
+    if (pthread_create(&th[t], 0, sworker, &jobs[t]) != 0) return -3.0;
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

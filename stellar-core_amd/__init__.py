@@ -67,7 +67,7 @@ EXPORTED_SYMBOLS = (
 )
 
 # test knobs (include/stellar_sigverify.h sv_set_debug_flags)
-DBG_TRIVIAL_PAIR, DBG_MAX_WINDOWS, DBG_FAIL = 0x1, 0x2, 0x4
+DBG_TRIVIAL_PAIR, DBG_MAX_WINDOWS, DBG_FAIL, DBG_PREP_ONLY = 0x1, 0x2, 0x4, 0x8
 
 
 class SigVerifyError(RuntimeError):

@@ -496,10 +496,30 @@ SV_HD void fe_sq2(fe& h, const fe& f) {
 #endif
   SV_FENCE();
 }
-// n successive squarings (rolled loop: keeps the code object small)
+// n successive squarings (rolled loop: keeps the code object small).  Two
+// squarings per iteration (SV_SQN_PAIRS): a product's outputs are early-clobber
+// registers distinct from its inputs, so a one-squaring loop copies its 10
+// limbs back into the loop-carried registers every iteration (10 v_mov per
+// squaring); with two the second squaring writes straight into them.
+#ifndef SV_SQN_PAIRS
+#define SV_SQN_PAIRS 1
+#endif
 SV_HD void fe_sqn(fe& h, const fe& f, int n) {
   fe_sq(h, f);
+#if SV_SQN_PAIRS
+  int i = 1;
+  if ((n - 1) & 1) {  // (n is a constant at every call site: folded)
+    fe_sq(h, h);
+    ++i;
+  }
+  SV_NOUNROLL for (; i < n; i += 2) {
+    fe t;
+    fe_sq(t, h);
+    fe_sq(h, t);
+  }
+#else
   SV_NOUNROLL for (int i = 1; i < n; ++i) fe_sq(h, h);
+#endif
 }
 
 // h = cond ? f : h  (per lane, branch-free)

@@ -186,7 +186,7 @@ std::atomic<uint32_t> g_dbg{0};          // sv_set_debug_flags
 std::atomic<size_t> g_min_shard{0};      // sv_set_min_shard (0: default)
 std::atomic<uint64_t> g_rr{0};           // round-robin slot for single-slot calls
 
-constexpr uint32_t kKernelDbgMask = SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS;
+constexpr uint32_t kKernelDbgMask = SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_PREP_ONLY;
 
 // Batches up to this size take the latency kernel under SV_PATH_AUTO
 // (measured crossover on MI355X).
@@ -972,7 +972,7 @@ int sv_set_kernel_path(int path) {
 }
 
 int sv_set_debug_flags(uint32_t flags) {
-  if (flags & ~(SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_FAIL)) return SV_ERR_INVALID_ARG;
+  if (flags & ~(SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_FAIL | SV_DBG_PREP_ONLY)) return SV_ERR_INVALID_ARG;
   return (int)g_dbg.exchange(flags);
 }
 

@@ -54,6 +54,7 @@ struct sv_kparams {
 // test knobs (include/stellar_sigverify.h sv_set_debug_flags)
 #define SV_DBG_TRIVIAL_PAIR 1u  // every lane takes the fallback pair (h, 1)
 #define SV_DBG_MAX_WINDOWS 2u   // every wave runs 64 windows
+#define SV_DBG_PREP_ONLY 8u     // split path: prep kernel only (profiling; no verdicts)
 __device__ __forceinline__ int sv_wave_windows(int wl, uint32_t dbg) {
   int W = (dbg & SV_DBG_MAX_WINDOWS) ? 64 : SV_LAT_MIN_WINDOWS;
   while (__ballot(wl > W) != 0) ++W;
@@ -918,7 +919,7 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
       hipLaunchKernelGGL(sv_prep_kernel<1>, dim3(pg), dim3(SV_BLOCK), 0, s, c);
     else
       hipLaunchKernelGGL(sv_prep_kernel<2>, dim3(pg), dim3(SV_BLOCK), 0, s, c);
-    hipLaunchKernelGGL(sv_main_kernel, dim3(grid < pg ? grid : pg), dim3(SV_BLOCK), 0, s, c);
+    if (!(dbg & SV_DBG_PREP_ONLY)) hipLaunchKernelGGL(sv_main_kernel, dim3(grid < pg ? grid : pg), dim3(SV_BLOCK), 0, s, c);
   }
 #elif SV_LATTICE
   if (mode == 0)

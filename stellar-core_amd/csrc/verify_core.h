@@ -791,10 +791,43 @@ SV_HD bool sv_is_identity(const ge_p3& P) {
 // Steps (1)-(5) of libsodium plus the decode of R (lattice.h), the Euclid
 // reduction and the table build.  Returns the pre-verdict and the lane's
 // window count in *W_lane; the caller picks the wave's W >= every W_lane.
+#ifndef SV_PREP_SEQ
+#define SV_PREP_SEQ 1
+#endif
 SV_COLD bool sv_lat_pre(sv_lat& lat, const uint32_t A[8], const uint32_t R[8], const uint32_t S[8],
                         const uint32_t hram[16], sv_u4* tabA, sv_u4* tabR, bool trivial = false) {
   bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
             sv_point_canonical(R);
+#if SV_PREP_SEQ == 2
+  // as below, with A and R through ONE copy of the decode + table code (a
+  // rolled loop: the inlined exponentiation chain is ~30 KB of code per copy)
+  uint32_t h[8];
+  sc_reduce512(h, hram);
+  SV_NOUNROLL for (int k = 0; k < 2; ++k) {
+    uint32_t w[8];
+    SV_UNROLL for (int i = 0; i < 8; ++i) w[i] = k ? R[i] : A[i];
+    ge_p3 negP;
+    ok = ge_frombytes(negP, w, true) && ok;
+    sv_build_ltab(k ? tabR : tabA, negP);
+  }
+  sc_lattice_reduce(lat, h, trivial);
+#elif SV_PREP_SEQ
+  // one point live at a time: h first (hram dies), then decode + table of -A,
+  // of -R, then the Euclid reduction with no point live
+  uint32_t h[8];
+  sc_reduce512(h, hram);
+  {
+    ge_p3 negA;
+    ok = ge_frombytes(negA, A, true) && ok;
+    sv_build_ltab(tabA, negA);
+  }
+  {
+    ge_p3 negR;
+    ok = ge_frombytes(negR, R, true) && ok;
+    sv_build_ltab(tabR, negR);
+  }
+  sc_lattice_reduce(lat, h, trivial);
+#else
   ge_p3 negA, negR;
   ok = ge_frombytes(negA, A, true) && ok;
   ok = ge_frombytes(negR, R, true) && ok;
@@ -803,5 +836,6 @@ SV_COLD bool sv_lat_pre(sv_lat& lat, const uint32_t A[8], const uint32_t R[8], c
   sc_lattice_reduce(lat, h, trivial);
   sv_build_ltab(tabA, negA);
   sv_build_ltab(tabR, negR);
+#endif
   return ok;
 }

@@ -38,24 +38,43 @@ sig[::8, 3] ^= 1
 torch.cuda.synchronize()
 want = None
 res = {k: [] for k in libs}
-for rnd in range(4):
+prep = {k: [] for k in libs}
+SV_DBG_PREP_ONLY = 0x8  # (include/stellar_sigverify.h)
+
+
+def timed(lib, out, reps=3):
+    lib.sv_timing_enable(1)
+    lib.sv_kernel_time_reset()
+    for _ in range(reps):
+        assert lib.sv_ed25519_verify_device(0, vp(pk.data_ptr()), vp(sig.data_ptr()), vp(msgs.data_ptr()), None,
+                                            None, 32, ctypes.c_size_t(n), vp(out.data_ptr()), None, None) == 0
+    lib.sv_device_synchronize(0)
+    ms, la, sg = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint64()
+    lib.sv_kernel_time(0, ctypes.byref(ms), ctypes.byref(la), ctypes.byref(sg))
+    lib.sv_timing_enable(0)
+    return ms.value / la.value
+
+
+ROUNDS = int(os.environ.get("AB_ROUNDS", "6"))
+for rnd in range(ROUNDS):
     for name, lib in libs.items():
         out = torch.zeros(n, dtype=torch.uint8, device=dev)
-        lib.sv_timing_enable(1)
-        lib.sv_kernel_time_reset()
-        for _ in range(3):
-            assert lib.sv_ed25519_verify_device(0, vp(pk.data_ptr()), vp(sig.data_ptr()), vp(msgs.data_ptr()), None,
-                                                None, 32, ctypes.c_size_t(n), vp(out.data_ptr()), None, None) == 0
-        lib.sv_device_synchronize(0)
-        ms, la, sg = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint64()
-        lib.sv_kernel_time(0, ctypes.byref(ms), ctypes.byref(la), ctypes.byref(sg))
-        lib.sv_timing_enable(0)
+        t = timed(lib, out)
         o = out.cpu().numpy()
         if want is None:
             want = o
             assert o.sum() == n - n // 8, o.sum()
         assert (o == want).all(), name + " verdict mismatch"
-        res[name].append(ms.value / la.value)
-        print("round %d %-28s %.3f ms" % (rnd, name, ms.value / la.value), flush=True)
+        has_split = hasattr(lib, "sv_set_debug_flags") and lib.sv_set_debug_flags(SV_DBG_PREP_ONLY) >= 0
+        tp = float("nan")
+        if has_split:
+            tp = timed(lib, torch.zeros(n, dtype=torch.uint8, device=dev))
+            lib.sv_set_debug_flags(0)
+        if rnd > 0:  # round 0 warms clocks and caches
+            res[name].append(t)
+            prep[name].append(tp)
+        print("round %d %-28s %.3f ms  (prep %.3f)" % (rnd, name, t, tp), flush=True)
 for name, v in res.items():
-    print("%-28s median %.3f ms per 2^20  (%.3e verifies/s)" % (name, float(np.median(v)), n / (np.median(v) * 1e-3)))
+    mp = float(np.median(prep[name]))
+    print("%-28s median %.3f ms per 2^20  (%.3e verifies/s)  prep %.3f  main %.3f" %
+          (name, float(np.median(v)), n / (np.median(v) * 1e-3), mp, float(np.median(v)) - mp))
