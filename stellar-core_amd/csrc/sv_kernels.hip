@@ -15,6 +15,8 @@
 // wave-interleaved layout measured ~4x more L2-miss traffic, profiles/r01/).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "verify_core.h"
 #include "quad.h"
 
@@ -787,11 +789,99 @@ int sv_debug_phase_cycles(unsigned long long out[8], int reset) {
 #endif
 
 size_t sv_ws_bytes_per_block(void) { return (size_t)SV_BLOCK * SV_SLOT_QUADS * sizeof(sv_u4); }
+
+// ------------------------------------------------- chunk planner (split path)
+// sv_main_kernel is persistent: Cm = CUs x blocks/CU x 4 resident waves, each
+// walking 64-signature groups with stride Cm, so a chunk of g groups runs
+// floor(g / Cm) full rounds and a last round of g mod Cm waves, dispatched one
+// block per CU first: d = ceil((g mod Cm) / SIMDs) waves per SIMD.  A SIMD
+// with fewer waves issues less per cycle (a wave's dependent issue leaves
+// gaps), measured on MI355X (profiles/r02/ab_chunk.txt): relative throughput
+// 0.55 with one wave, 0.97 with two, against the main kernel's three.  So a
+// 2^20 batch in one chunk (16384 groups = 5 rounds + a last round of one wave
+// per SIMD) loses ~4 % against two chunks of 8192 (2 rounds + two waves per
+// SIMD each).  The planner splits a launch into k equal chunks (k from the
+// workspace bound up) minimising the modelled time of both kernels.
+static double sv_rounds(uint64_t g, uint64_t simds, int wps) {
+  const uint64_t C = simds * (uint64_t)wps;
+  const uint64_t full = g / C, rem = g % C;
+  double t = (double)full;
+  if (rem) {
+    const uint64_t d = (rem + simds - 1) / simds;  // waves per SIMD in the last round
+    const double eff = d >= (uint64_t)wps ? 1.0 : (d == 1 ? 0.55 : 0.97);
+    t += (double)d / ((double)wps * eff);
+  }
+  return t;
+}
+// resident waves per SIMD of a kernel (occupancy API; cached, benign races)
+static int sv_wps(const void* kernel, std::atomic<int>& cache) {
+  int w = cache.load(std::memory_order_relaxed);
+  if (w == 0) {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, SV_BLOCK, 0) != hipSuccess || b < 1) b = 1;
+    w = b * (SV_BLOCK / 64) / 4;
+    if (w < 1) w = 1;
+    cache.store(w, std::memory_order_relaxed);
+  }
+  return w;
+}
+static std::atomic<int> g_main_wps{0}, g_prep_wps{0};
+static int sv_main_wps(void) { return sv_wps((const void*)sv_main_kernel, g_main_wps); }
+static int sv_prep_wps(void) { return sv_wps((const void*)sv_prep_kernel<0>, g_prep_wps); }
+// SIMDs of the current device (4 per CU)
+static std::atomic<int> g_cus[64];
+static uint64_t sv_device_simds(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  int c = g_cus[dev].load(std::memory_order_relaxed);
+  if (c == 0) {
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1) return 0;
+    g_cus[dev].store(c, std::memory_order_relaxed);
+  }
+  return 4u * (uint64_t)c;
+}
+// Signatures per chunk for a throughput-path launch of n on the current
+// device (every chunk but the last has exactly this many; a multiple of 64,
+// at most SV_CHUNK).
+#ifndef SV_PLAN
+#define SV_PLAN 1  // 0: fixed SV_CHUNK-signature chunks (A/B baseline)
+#endif
+uint64_t sv_plan_chunk(uint64_t n) {
+  if (!SV_PLAN) return SV_CHUNK;
+  const uint64_t G = (n + 63) / 64;
+  const uint64_t capG = SV_CHUNK / 64;
+  const int mw = sv_main_wps(), pw = sv_prep_wps();
+  const uint64_t simds = sv_device_simds();
+  if (G == 0 || simds == 0) return SV_CHUNK;
+  const uint64_t kmin = (G + capG - 1) / capG;
+  // per-group costs: main round of Cm groups vs prep round of Cp groups, in
+  // main-group units (MI355X: 0.45 us vs 0.17 us per group); launch pair ~ 20
+  const double kPrep = 0.38, kLaunch = 20.0;
+  uint64_t best_k = kmin;
+  double best = 0.0;
+  for (uint64_t k = kmin; k <= 2 * kmin + 4 && k <= G; ++k) {
+    const uint64_t g = (G + k - 1) / k, last = G - (k - 1) * g;
+    if (last == 0 || last > g) continue;
+    const double one = sv_rounds(g, simds, mw) * (double)(simds * mw) +
+                       kPrep * sv_rounds(g, simds, pw) * (double)(simds * pw);
+    const double tail = sv_rounds(last, simds, mw) * (double)(simds * mw) +
+                        kPrep * sv_rounds(last, simds, pw) * (double)(simds * pw);
+    const double t = (double)(k - 1) * one + tail + kLaunch * (double)k;
+    if (k == kmin || t < best * 0.999) {
+      best = t;
+      best_k = k;
+    }
+  }
+  const uint64_t g = (G + best_k - 1) / best_k;
+  return g * 64 < SV_CHUNK ? g * 64 : SV_CHUNK;
+}
+
 // Signatures one throughput-path launch sequence processes per prep/main
-// chunk: the workspace of a batch of n holds ws_cap(n) = min(n, SV_CHUNK)
+// chunk (sv_plan_chunk): the workspace of a batch of n holds ws_cap(n) of them,
 // rounded up to whole workgroups.
 uint64_t sv_ws_cap(uint64_t n) {
-  const uint64_t c = n < SV_CHUNK ? n : SV_CHUNK;
+  const uint64_t p = sv_plan_chunk(n);
+  const uint64_t c = n < p ? n : p;
   return (c + SV_BLOCK - 1) / SV_BLOCK * SV_BLOCK;
 }
 // Device workspace for `grid` persistent workgroups (fused verify kernel,
@@ -903,13 +993,14 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
   (void)path;
 #if SV_LATTICE && SV_SPLIT
   const uint64_t cap = sv_ws_cap(n);
+  const uint64_t chunk = sv_plan_chunk(n);
   sv_u4* rec = p.ws + (size_t)cap * SV_SLOT_QUADS_L;
   uint32_t* wmax = (uint32_t*)(rec + (size_t)cap * SV_REC_QUADS);
-  for (uint64_t start = 0; start < n; start += cap) {
+  for (uint64_t start = 0; start < n; start += chunk) {
     sv_cparams c;
     c.k = p;
     c.start = start;
-    c.cnt = n - start < cap ? n - start : cap;
+    c.cnt = n - start < chunk ? n - start : chunk;
     c.rec = rec;
     c.wmax = wmax;
     const unsigned pg = (unsigned)((c.cnt + SV_BLOCK - 1) / SV_BLOCK);

@@ -23,6 +23,8 @@ for p in paths:
     print("%-28s resident workgroups/CU: %d" % (os.path.basename(p), lib.sv_occupancy_blocks_per_cu()), flush=True)
 
 dev = torch.device("cuda", 0)
+_pr = torch.cuda.get_device_properties(0)
+print("device %s CUs %d" % (_pr.name, _pr.multi_processor_count), flush=True)
 n = 1 << 20
 g = torch.Generator(device="cpu").manual_seed(5)
 seeds = torch.randint(0, 256, (n, 32), dtype=torch.uint8, generator=g).to(dev)
