@@ -34,6 +34,11 @@
 struct fe {
   uint32_t v[10];
 };
+// 19 g[1..9] of a product's g operand, computed once when two products share
+// g (fe_mul_g19)
+struct fe19 {
+  uint32_t v[9];
+};
 
 #define SV_M26 0x3ffffffu
 #define SV_M25 0x1ffffffu
@@ -90,6 +95,19 @@ SV_HD void fe_weak(fe& h) {
   }
   h.v[0] += 19u * c[9];
   SV_UNROLL for (int i = 1; i < 10; ++i) h.v[i] += c[i - 1];
+}
+
+// Carry of the even limbs 2, 4, 6, 8 only (into 3, 5, 7, 9): enough to use an
+// M5 value as a product's g operand.  g's limbs 1..9 are pre-multiplied by 19
+// (19 g_j < 2^32 needs g_even <= 3.37 2^26, g_odd <= 6.7 2^25; limb 0 never is),
+// so after this even limbs are R and odd ones <= 5 2^25 + 5; the column sums
+// stay < 2^63 with an M5 f operand (tests/test_host_arith.py fuzzes it).
+SV_HD void fe_weak_even(fe& h) {
+  SV_UNROLL for (int i = 2; i < 10; i += 2) {
+    const uint32_t c = h.v[i] >> 26;
+    h.v[i] &= SV_M26;
+    h.v[i + 1] += c;
+  }
 }
 
 // Sequential carry of 64-bit column sums into a carried fe (R).
@@ -455,6 +473,20 @@ SV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   uint64_t c[10];
   fe_mul_cols<false>(c, f, g);
   fe_carry_wide(h, c);
+#endif
+  SV_FENCE();
+}
+SV_HD void fe_premul19(fe19& t, const fe& g) {
+  SV_UNROLL for (int j = 1; j < 10; ++j) t.v[j - 1] = 19u * g.v[j];
+}
+// h = f g with t = fe_premul19(g) (same value and bounds as fe_mul)
+SV_HD void fe_mul_g19(fe& h, const fe& f, const fe& g, const fe19& t) {
+#if SV_FE_ASM_ON
+  fe_mul_g19_asm(h, f, g, t);
+#else
+  (void)t;
+  fe_mul(h, f, g);
+  return;
 #endif
   SV_FENCE();
 }

@@ -68,6 +68,9 @@ SV_HD void fe_weak(fe& h) {
   h.l[0] += 19 * c[4];
   for (int i = 1; i < 5; ++i) h.l[i] += c[i - 1];
 }
+// (radix 2^51: every limb carried, as fe_weak; the device form carries the
+// even limbs only)
+SV_HD void fe_weak_even(fe& h) { fe_weak(h); }
 
 // column sums (< 2^120) -> R; the carries stay 128-bit
 SV_HD void fe51_carry(fe& h, sv_u128 r0, sv_u128 r1, sv_u128 r2, sv_u128 r3, sv_u128 r4) {
@@ -101,6 +104,18 @@ SV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   fe51_carry(h, r0, r1, r2, r3, r4);
 }
 // h = 2 f g
+// (device form: a product with the 19-multiples of g given; here nothing to share)
+struct fe19 {
+  int unused;
+};
+SV_HD void fe_premul19(fe19& t, const fe& g) {
+  (void)g;
+  t.unused = 0;
+}
+SV_HD void fe_mul_g19(fe& h, const fe& f, const fe& g, const fe19& t) {
+  (void)t;
+  fe_mul(h, f, g);
+}
 SV_HD void fe_mul2(fe& h, const fe& f, const fe& g) {
   fe f2;
   for (int i = 0; i < 5; ++i) f2.l[i] = f.l[i] << 1;

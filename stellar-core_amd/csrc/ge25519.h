@@ -24,6 +24,13 @@
 #include "fe25519.h"
 
 
+#ifndef SV_DBL_WEAK_EVEN
+#define SV_DBL_WEAK_EVEN 1
+#endif
+#ifndef SV_SHARE_T19
+#define SV_SHARE_T19 1
+#endif
+
 struct ge_p2 { fe X, Y, Z; };
 struct ge_p3 { fe X, Y, Z, T; };
 struct ge_p1p1 { fe X, Y, Z, T; };
@@ -51,20 +58,42 @@ SV_HD void ge_dbl(ge_p1p1& r, const fe& X, const fe& Y, const fe& Z) {
   fe_add(r.Y, YY, XX);    // y^2 + x^2            M2
   fe_sub(r.Z, YY, XX);    // y^2 - x^2            M3
   fe_sub4(r.X, AA, r.Y);  // 2xy = (x+y)^2 - ..  M5
-  fe_sub4(r.T, ZZ2, r.Z); // 2z^2 - (y^2 - x^2)  M5 -> R+
-  fe_weak(r.T);
+  fe_sub4(r.T, ZZ2, r.Z); // 2z^2 - (y^2 - x^2)  M5
+#if SV_DBL_WEAK_EVEN
+  fe_weak_even(r.T);      // T is only ever a conversion product's g operand
+#else
+  fe_weak(r.T);           // R+
+#endif
 }
 
+// T is the g operand of two conversion products: its 19-multiples are
+// computed once (SV_SHARE_T19)
 SV_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
+#if SV_SHARE_T19
+  fe19 t19;
+  fe_premul19(t19, p.T);
+  fe_mul_g19(r.X, p.X, p.T, t19);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul_g19(r.Z, p.Z, p.T, t19);
+#else
   fe_mul(r.X, p.X, p.T);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
+#endif
 }
 
 SV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
+#if SV_SHARE_T19
+  fe19 t19;
+  fe_premul19(t19, p.T);
+  fe_mul_g19(r.X, p.X, p.T, t19);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul_g19(r.Z, p.Z, p.T, t19);
+#else
   fe_mul(r.X, p.X, p.T);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
+#endif
   fe_mul(r.T, p.X, p.Y);
 }
 
@@ -73,9 +102,17 @@ SV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
 // matters: p.X (up to M5 after a doubling) is always the f operand.
 SV_HD void ge_p1p1_to_p3_opt(ge_p3& r, const ge_p1p1& p, bool wantT) {
   if (wantT) fe_mul(r.T, p.X, p.Y);
+#if SV_SHARE_T19
+  fe19 t19;
+  fe_premul19(t19, p.T);
+  fe_mul_g19(r.X, p.X, p.T, t19);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul_g19(r.Z, p.Z, p.T, t19);
+#else
   fe_mul(r.X, p.X, p.T);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
+#endif
 }
 
 // r = p + q where the caller has already swapped q's (Y+X, Y-X) pair for a

@@ -78,7 +78,11 @@ __device__ __forceinline__ void qd_dbl(ge_p3& P, const qd_role& q, bool wantT) {
   fe_sub(r.Z, YY, XX);
   fe_sub4(r.X, AA, r.Y);
   fe_sub4(r.T, ZZ2, r.Z);
+#if SV_DBL_WEAK_EVEN
+  fe_weak_even(r.T);  // (T: a conversion product's g operand only)
+#else
   fe_weak(r.T);
+#endif
   qd_p1p1_to_p3(P, r, q, wantT);
 }
 

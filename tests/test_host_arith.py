@@ -83,6 +83,23 @@ def test_fe_mul_m5_f_operand(hostcore):
         assert _words(o) == _val(lf) * _val(lg) % P
 
 
+def test_fe_mul_partial_carry_g_operand(hostcore):
+    """ge_dbl leaves T at M5 and carries only its even limbs 2..8
+    (fe_weak_even): T is then the g operand of the conversion products X*T
+    (X at M5) and Z*T, with g limb 0 up to M5 and odd limbs up to 5 2^25 + 5."""
+    rnd = random.Random(11)
+    o = (ctypes.c_uint32 * 8)()
+    gmax = [5 * (1 << 26) - 1] + [(1 << 26) - 1 if j % 2 == 0 else 5 * (1 << 25) + 5 for j in range(1, 10)]
+    for trial in range(400):
+        if trial < 10:
+            lf, lg = [5 * (1 << w) - 1 for w in W], list(gmax)
+        else:
+            lf = [rnd.randrange(5 * (1 << w)) for w in W]
+            lg = [rnd.randrange(m + 1) for m in gmax]
+        hostcore.hc_fe_mul_limbs(o, (ctypes.c_uint32 * 10)(*lf), (ctypes.c_uint32 * 10)(*lg), 0)
+        assert _words(o) == _val(lf) * _val(lg) % P
+
+
 def test_fe_tobytes_edge_values(hostcore):
     o = (ctypes.c_uint32 * 8)()
     for v in [0, 1, P - 1, P, P + 1, P + 18, 2**255 - 1, 2 * P - 1]:

@@ -28,9 +28,9 @@ MASK = ["0x3ffffff" if w == 26 else "0x1ffffff" for w in WIDTH]
 CLOB = ", ".join('"v%d"' % r for r in range(0, 4)) + ", " + ", ".join('"s%d"' % r for r in range(88, 96))
 
 
-def product(name, terms_of_col, temps, inputs, doc):
+def product(name, terms_of_col, temps, inputs, doc, sig=None):
     """terms_of_col[k] = list of (a_operand, b_operand) names; temps = list of
-    (name, instruction text producing it)."""
+    (name, instruction text producing it); sig: explicit parameter list."""
     lines = []
     for _, text in temps:
         lines.append(text)
@@ -67,7 +67,8 @@ def product(name, terms_of_col, temps, inputs, doc):
     body = "\n".join('      "%s\\n"' % l for l in lines)
     out = []
     out.append("// %s" % doc)
-    out.append("SV_HD void %s(fe& h, %s) {" % (name, ", ".join("const fe& " + v for v in sorted({e.split('.')[0] for _, e in inputs}))))
+    params = sig or ", ".join("const fe& " + v for v in sorted({e.split('.')[0] for _, e in inputs}))
+    out.append("SV_HD void %s(fe& h, %s) {" % (name, params))
     out.append("  uint32_t o[10];")
     for n, _ in temps:
         out.append("  uint32_t %s;" % n)
@@ -81,11 +82,16 @@ def product(name, terms_of_col, temps, inputs, doc):
     return "\n".join(out)
 
 
-def gen_mul(dbl):
+def gen_mul(dbl, pre19=False):
+    """pre19: the 19-multiples of g's limbs 1..9 come in as g19 (fe19), so a g
+    shared by two products is pre-multiplied once (ge_p1p1_to_p3's T)."""
     inputs = [("f%d" % i, "f.v[%d]" % i) for i in range(10)] + [("g%d" % j, "g.v[%d]" % j) for j in range(10)]
     temps = []
     for j in range(1, 10):
-        temps.append(("t19_%d" % j, "v_mul_lo_u32 %%[t19_%d], %%[g%d], 19" % (j, j)))
+        if pre19:
+            inputs.append(("t19_%d" % j, "g19.v[%d]" % (j - 1)))
+        else:
+            temps.append(("t19_%d" % j, "v_mul_lo_u32 %%[t19_%d], %%[g%d], 19" % (j, j)))
     fa = {}
     fb = {}
     for i in range(10):
@@ -106,8 +112,11 @@ def gen_mul(dbl):
             b = "t19_%d" % j if i + j >= 10 else "g%d" % j
             col.append((a, b))
         cols.append(col)
-    name = "fe_mul2_asm" if dbl else "fe_mul_asm"
+    name = ("fe_mul2_asm" if dbl else "fe_mul_asm") if not pre19 else "fe_mul_g19_asm"
     doc = "h = %sf g (fe_mul_cm<%s>)" % ("2 " if dbl else "", "true" if dbl else "false")
+    if pre19:
+        doc += ", g19 = 19 g[1..9] given"
+        return product(name, cols, temps, inputs, doc, sig="const fe& f, const fe& g, const fe19& g19")
     return product(name, cols, temps, inputs, doc)
 
 
@@ -154,7 +163,7 @@ def main():
     print("// fe_mul_cm / fe_sq_cm there, which the host build and tests/ exercise.")
     print("#pragma once")
     print()
-    for f in (gen_mul(False), gen_mul(True), gen_sq(False), gen_sq(True)):
+    for f in (gen_mul(False), gen_mul(True), gen_sq(False), gen_sq(True), gen_mul(False, pre19=True)):
         print(f)
         print()
 
