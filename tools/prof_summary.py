@@ -28,6 +28,18 @@ def main():
         batch = int(sys.argv[sys.argv.index("--batch") + 1])
     out = {"profile_dir": d, "batch": batch}
     pat = re.compile(r"sv_verify(_lat)?_kernel<0>|sv_prep_kernel<0>|sv_main_kernel")
+    # the throughput path may cut one launch into several equal chunks
+    # (sv_plan_chunk): chunk size = the prep kernel's grid (one lane per
+    # signature), and a launch's value = per-dispatch value x chunks
+    chunks = 1
+    for f in glob.glob(os.path.join(d, "*", "*_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if "sv_prep_kernel<0>" in r["Kernel_Name"] and int(r["Grid_Size"]) >= 1024:
+                chunks = max(1, batch // int(r["Grid_Size"]))
+                break
+        if chunks > 1:
+            break
+    out["chunks_per_launch"] = chunks
     ks = glob.glob(os.path.join(d, "kt", "*_kernel_stats.csv"))
     if ks:
         per = {}
@@ -38,10 +50,10 @@ def main():
         if per:
             out["kernel"] = " + ".join(sorted(per))
             out["kernels"] = per
-            out["calls"] = min(v["calls"] for v in per.values())
-            # one verify launch = one dispatch of each kernel of the path
+            out["calls"] = min(v["calls"] for v in per.values()) // chunks
+            # one verify launch = `chunks` dispatches of each kernel of the path
             for k in ("avg_ns", "min_ns", "max_ns"):
-                out[k] = sum(v[k] for v in per.values())
+                out[k] = chunks * sum(v[k] for v in per.values())
     # per kernel: counter -> list over dispatches; a launch's value = sum over the path's kernels
     vals = defaultdict(lambda: defaultdict(list))
     meta = {}
@@ -57,7 +69,7 @@ def main():
     avg = defaultdict(float)
     per_kernel = {}
     for kn, cv in vals.items():
-        per_kernel[kn] = {c: sum(v) / len(v) for c, v in cv.items()}
+        per_kernel[kn] = {c: chunks * sum(v) / len(v) for c, v in cv.items()}
         for c, a in per_kernel[kn].items():
             avg[c] += a
     avg = dict(avg)
