@@ -618,27 +618,61 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
   SV_UNROLL for (int i = 0; i < 10; ++i) o.v[i] = oc_from_hi(f.v[i]);
 }
 
+#ifndef SV_LAT_SPLIT
+#define SV_LAT_SPLIT 1
+#endif
+#define SV_OCTET_BLOCK (SV_LAT_SPLIT ? 128 : 64)
+
 template <int MODE>
-__global__ __launch_bounds__(64, 1) void sv_octet_kernel(sv_kparams p) {
+__global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams p) {
   __shared__ uint32_t s_tab[SV_OSIGS][2][SV_ATAB_ENTRIES][SV_QENT_DW];  // 23 KB
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
   const uint32_t role = lane & 3u, half = (lane >> 2) & 1u, sl = lane >> 3;
   const qd_role q{role == 1, role == 2, role == 3};
   const uint64_t i = (uint64_t)blockIdx.x * SV_OSIGS + sl;
   const bool active = i < p.n;
   const uint64_t ii = active ? i : p.n - 1;  // idle tail octets redo the last item
+#if SV_LAT_SPLIT
+  // Two waves per workgroup, same lane -> (signature, quad, role) map.  The
+  // decompressions and table builds (wave 1) do not depend on the hash, the
+  // scalar reduction and the Euclid reduction (wave 0), so the two chains run
+  // side by side on two SIMDs instead of one after the other; wave 1 hands
+  // over the tables in LDS (as before) and its decode verdicts in s_dok.
+  __shared__ uint32_t s_dok[SV_OSIGS];
+  // wave-uniform, and visibly so to the compiler (a scalar branch): a
+  // divergent-looking branch would be structurized with EXEC masking and
+  // both waves would then execute both barriers
+  const bool dec_wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0;
+  uint32_t A[8], S[8], hram[16], R[8];
+  if (dec_wave) {
+    sv_unpack2(A, p.pk + 2 * ii);
+    sv_unpack2(R, p.sig + 4 * ii);
+  } else {
+    sv_load_and_hash<MODE>(p, ii, A, S, hram);
+    sv_unpack2(R, p.sig + 4 * ii);
+  }
+  bool ok = true;
+  if (dec_wave) {
+#else
   uint32_t A[8], S[8], hram[16], R[8];
   sv_load_and_hash<MODE>(p, ii, A, S, hram);
   sv_unpack2(R, p.sig + 4 * ii);
   bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
             sv_point_canonical(R);
   {
+#endif
     // decompress: quad 0 -A, quad 1 -R; role 0 of each quad stores its table
     uint32_t E[8];
     SV_UNROLL for (int k = 0; k < 8; ++k) E[k] = half ? R[k] : A[k];
     ge_p3 Pt;
     const uint32_t dok = ge_frombytes(Pt, E, true) ? 1u : 0u;
+#if SV_LAT_SPLIT
+    // (the DPP read outside the branch: a lane disabled by EXEC is no source)
+    const uint32_t both = dok & oc_from_hi(dok);
+    if (half == 0 && role == 0) s_dok[sl] = both;
+#else
     ok = ok && (dok & oc_from_hi(dok)) != 0;  // (valid on quad 0, the lanes that use it)
+#endif
     ge_cached c1, ce;
     ge_p3_to_cached(c1, Pt);
     ge_cached_identity(ce);
@@ -658,6 +692,14 @@ __global__ __launch_bounds__(64, 1) void sv_octet_kernel(sv_kparams p) {
       if (store) sv_store_lentry((sv_u4*)(tab + e * SV_QENT_DW), ce);
     }
   }
+#if SV_LAT_SPLIT
+  if (dec_wave) {
+    __syncthreads();  // tables and s_dok written
+    return;
+  }
+  ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
+       sv_point_canonical(R);
+#endif
   sv_lat lat;
   {
     uint32_t h[8];
@@ -668,6 +710,9 @@ __global__ __launch_bounds__(64, 1) void sv_octet_kernel(sv_kparams p) {
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
   __syncthreads();  // tables visible to the whole quad
+#if SV_LAT_SPLIT
+  ok = ok && s_dok[sl] != 0;
+#endif
 
   const sv_u4* btab = p.btab + (half ? SV_LBTAB_ENTRIES * SV_BTAB_QUADS : 0);
   const uint32_t* tab = &s_tab[sl][half][0][0];
@@ -973,11 +1018,11 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
 #if SV_LAT_OCTET
     const unsigned og = (unsigned)((n + SV_OSIGS - 1) / SV_OSIGS);
     if (mode == 0)
-      hipLaunchKernelGGL(sv_octet_kernel<0>, dim3(og), dim3(64), 0, s, p);
+      hipLaunchKernelGGL(sv_octet_kernel<0>, dim3(og), dim3(SV_OCTET_BLOCK), 0, s, p);
     else if (mode == 1)
-      hipLaunchKernelGGL(sv_octet_kernel<1>, dim3(og), dim3(64), 0, s, p);
+      hipLaunchKernelGGL(sv_octet_kernel<1>, dim3(og), dim3(SV_OCTET_BLOCK), 0, s, p);
     else
-      hipLaunchKernelGGL(sv_octet_kernel<2>, dim3(og), dim3(64), 0, s, p);
+      hipLaunchKernelGGL(sv_octet_kernel<2>, dim3(og), dim3(SV_OCTET_BLOCK), 0, s, p);
 #else
     const unsigned qg = (unsigned)((n + SV_QSIGS - 1) / SV_QSIGS);
     if (mode == 0)

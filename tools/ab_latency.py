@@ -32,9 +32,31 @@ first = next(iter(libs.values()))
 assert first.sv_ed25519_sign_device(0, vp(seeds.data_ptr()), vp(msgs.data_ptr()), ctypes.c_size_t(n),
                                     vp(pk.data_ptr()), vp(sig.data_ptr()), None) == 0
 first.sv_device_synchronize(0)
+# SCP-sized variable-length messages (128-384 B: 2-4 SHA-512 blocks), random
+# bytes: timing only (every lane runs every phase whatever its verdict)
+rng = np.random.default_rng(9)
+vlen = rng.integers(128, 385, n).astype(np.uint32)
+voff = np.zeros(n, np.uint64)
+voff[1:] = np.cumsum(vlen[:-1], dtype=np.uint64)
+vmsg = torch.from_numpy(rng.integers(0, 256, int(vlen.sum()), dtype=np.uint8)).to(dev)
+voff_d = torch.from_numpy(voff.view(np.int64)).to(dev)
+vlen_d = torch.from_numpy(vlen.view(np.int32)).to(dev)
 res = {k: [] for k in libs}
+resv = {k: [] for k in libs}
 for rnd in range(5):
     for name, lib in libs.items():
+        out = torch.zeros(n, dtype=torch.uint8, device=dev)
+        lib.sv_timing_enable(1)
+        lib.sv_kernel_time_reset()
+        for _ in range(20):
+            assert lib.sv_ed25519_verify_device(0, vp(pk.data_ptr()), vp(sig.data_ptr()), vp(vmsg.data_ptr()),
+                                                vp(voff_d.data_ptr()), vp(vlen_d.data_ptr()), 0, ctypes.c_size_t(n),
+                                                vp(out.data_ptr()), None, None) == 0
+        lib.sv_device_synchronize(0)
+        ms, la, sg = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint64()
+        lib.sv_kernel_time(0, ctypes.byref(ms), ctypes.byref(la), ctypes.byref(sg))
+        lib.sv_timing_enable(0)
+        resv[name].append(ms.value / la.value)
         out = torch.zeros(n, dtype=torch.uint8, device=dev)
         lib.sv_timing_enable(1)
         lib.sv_kernel_time_reset()
@@ -49,4 +71,5 @@ for rnd in range(5):
         if rnd == 0:
             print("%-28s valid rows %d" % (name, int(out.sum().item())), flush=True)
 for name, v in res.items():
-    print("%-28s median %.4f ms per 1k batch (latency path)" % (name, float(np.median(v))), flush=True)
+    print("%-28s median %.4f ms per 1k batch (latency path, 32 B)  %.4f ms (128-384 B)"
+          % (name, float(np.median(v)), float(np.median(resv[name]))), flush=True)
