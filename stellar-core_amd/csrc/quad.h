@@ -113,3 +113,124 @@ __device__ __forceinline__ void qd_add(ge_p3& P, const fe& mine, const qd_role& 
   }
   qd_p1p1_to_p3(P, r, q, wantT);
 }
+
+// ---------------------------------------------------------------------------
+// "Own form" (the latency kernels' scalar-multiplication loop): lane r of the
+// quad holds ONLY coordinate r of P (0 X, 1 Y, 2 Z, 3 T) -- the product it
+// computed last -- instead of the whole point.  Each step moves just the
+// values its lanes need (DPP quad_perm with per-lane sources) instead of
+// broadcasting every result to every lane and picking from four, and the
+// conversion products keep a fixed lane map (X, Y, Z, T on lanes 0..3), so
+// no step ever rebuilds the whole point until the end (qo_expand).  Same
+// field operations, operand order and bounds as ge_dbl / ge_add_preswapped /
+// ge_p1p1_to_p3 (ge25519.h), hence the same verdicts.
+
+// value of lane P<r> of this lane's quad, for lane r
+template <int P0, int P1, int P2, int P3>
+__device__ __forceinline__ void fe_perm(fe& o, const fe& f) {
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    o.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)f.v[i], P0 | (P1 << 2) | (P2 << 4) | (P3 << 6), 0xf, 0xf,
+                                               false);
+#else
+    o.v[i] = f.v[i];
+#endif
+  }
+}
+
+// P = identity: (0 : 1 : 1 : 0)
+__device__ __forceinline__ void qo_identity(fe& h, const qd_role& q) {
+  if (q.r1 || q.r2) fe_1(h);
+  else fe_0(h);
+}
+
+// the whole point on every lane of the quad
+__device__ __forceinline__ void qo_expand(ge_p3& P, const fe& h) {
+  fe_from<0>(P.X, h);
+  fe_from<1>(P.Y, h);
+  fe_from<2>(P.Z, h);
+  fe_from<3>(P.T, h);
+}
+
+// P = 2P: lanes 0, 1, 2 square their own coordinate (lane 2 doubles it),
+// lane 3 squares X + Y; the conversion products X'T', Y'Z', Z'T', X'Y' land
+// on lanes 0..3 again.
+__device__ __forceinline__ void qo_dbl(fe& h, const qd_role& q) {
+  fe x, y, s, sq;
+  fe_from<0>(x, h);
+  fe_from<1>(y, h);
+  fe_add(s, x, y);  // X + Y (M2)
+  SV_UNROLL for (int i = 0; i < 10; ++i) s.v[i] = q.r3 ? s.v[i] : h.v[i];
+  fe_sq(sq, s);
+  if (q.r2) fe_add(sq, sq, sq);  // 2 Z^2 (M2; the bound ge_dbl's fe_sub4 below accepts)
+  fe XX, YY, u, w;
+  fe_from<0>(XX, sq);
+  fe_from<1>(YY, sq);
+  fe_perm<3, 1, 2, 3>(u, sq);  // lanes 0, 3: (X+Y)^2
+  fe_perm<2, 1, 2, 3>(w, sq);  // lanes 0, 2: 2 Z^2
+  fe Yp, Zp, Xp, Tp;
+  fe_add(Yp, YY, XX);   // y^2 + x^2            M2
+  fe_sub(Zp, YY, XX);   // y^2 - x^2            M3
+  fe_sub4(Xp, u, Yp);   // 2xy (lanes 0, 3)     M5
+  fe_sub4(Tp, w, Zp);   // (lanes 0, 2)         M5
+#if SV_DBL_WEAK_EVEN
+  fe_weak_even(Tp);  // (T: a conversion product's g operand only)
+#else
+  fe_weak(Tp);
+#endif
+  // lane 0 X'T', 1 Y'Z', 2 Z'T', 3 X'Y' (p1p1 X is always the f operand)
+  fe f, g;
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    f.v[i] = q.r1 ? Yp.v[i] : (q.r2 ? Zp.v[i] : Xp.v[i]);
+    g.v[i] = q.r3 ? Yp.v[i] : (q.r1 ? Zp.v[i] : Tp.v[i]);
+  }
+  fe_mul(h, f, g);
+}
+
+// this lane's operand of cached entry `ent` (LDS; YpX, YmX, Z, T2d x 10
+// dwords) in own-form roles: lane 0 the (Y+X) side, lane 1 the (Y-X) side
+// (swapped when neg), lane 2 Z, lane 3 2dT
+__device__ __forceinline__ void qo_load_cached(fe& o, const uint32_t* ent, uint32_t role, bool neg) {
+  const uint32_t comp = role >= 2 ? role : ((role == 0) != neg ? 0u : 1u);
+  const uint32_t* src = ent + 10 * comp;
+  SV_UNROLL for (int k = 0; k < 10; ++k) o.v[k] = src[k];
+}
+// the same for an affine base-point entry (global; y+x, y-x, 2dxy as 3 quads
+// each): lane 2 the constant 1 (Z)
+__device__ __forceinline__ void qo_load_affine(fe& o, const sv_u4* ent, uint32_t role, bool neg) {
+  const uint32_t comp = role == 3 ? 2u : role == 2 ? 0u : ((role == 0) != neg ? 0u : 1u);
+  const sv_u4* src = ent + 3 * comp;
+  const sv_u4 a = src[0], b = src[1], c = src[2];
+  o.v[0] = a.x; o.v[1] = a.y; o.v[2] = a.z; o.v[3] = a.w;
+  o.v[4] = b.x; o.v[5] = b.y; o.v[6] = b.z; o.v[7] = b.w;
+  o.v[8] = c.x; o.v[9] = c.y;
+  if (role == 2) fe_1(o);
+}
+
+// P += entry: lane 0 (Y+X)(Y'+X'), 1 (Y-X)(Y'-X'), 2 2Z Z', 3 T 2dT', then
+// the conversion products as in qo_dbl.  neg swaps the final Z/T pair.
+__device__ __forceinline__ void qo_add(fe& h, const fe& mine, const qd_role& q, bool neg) {
+  fe r, a, b, f, pr;
+  fe_perm<1, 0, 2, 3>(r, h);  // lane 0 <- Y, 1 <- X, 2 and 3 their own
+  fe_add(a, h, r);            // lane 0 X + Y, lane 2 2Z   M2
+  fe_sub(b, h, r);            // lane 1 Y - X              M3
+  SV_UNROLL for (int i = 0; i < 10; ++i) f.v[i] = q.r1 ? b.v[i] : (q.r3 ? h.v[i] : a.v[i]);
+  fe_mul(pr, f, mine);
+  fe PP, MM, ZZ, TT;
+  fe_from<0>(PP, pr);
+  fe_from<1>(MM, pr);
+  fe_from<2>(ZZ, pr);
+  fe_from<3>(TT, pr);
+  fe X1, Y1, zp, zm;
+  fe_sub(X1, PP, MM);  // M3
+  fe_add(Y1, PP, MM);  // M2
+  fe_add(zp, ZZ, TT);  // M2
+  fe_sub(zm, ZZ, TT);  // M3
+  fe g;
+  SV_UNROLL for (int i = 0; i < 10; ++i) {
+    const uint32_t z1 = neg ? zm.v[i] : zp.v[i], t1 = neg ? zp.v[i] : zm.v[i];
+    f.v[i] = q.r1 ? Y1.v[i] : (q.r2 ? z1 : X1.v[i]);
+    g.v[i] = q.r3 ? Y1.v[i] : (q.r1 ? z1 : t1);
+  }
+  fe_mul(h, f, g);
+}

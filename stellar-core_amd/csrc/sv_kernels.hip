@@ -621,6 +621,9 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
 #ifndef SV_LAT_SPLIT
 #define SV_LAT_SPLIT 1
 #endif
+#ifndef SV_LAT_OWN
+#define SV_LAT_OWN 1
+#endif
 #define SV_OCTET_BLOCK (SV_LAT_SPLIT ? 128 : 64)
 
 template <int MODE>
@@ -648,11 +651,21 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     sv_unpack2(A, p.pk + 2 * ii);
     sv_unpack2(R, p.sig + 4 * ii);
   } else {
+#ifdef SV_QPROF_NOHASH  // (developer A/B builds only: phase timing of this kernel)
+    sv_unpack2(A, p.pk + 2 * ii);
+    sv_unpack2(S, p.sig + 4 * ii + 2);
+    SV_UNROLL for (int k = 0; k < 16; ++k) hram[k] = A[k & 7] ^ (uint32_t)k;
+#else
     sv_load_and_hash<MODE>(p, ii, A, S, hram);
+#endif
     sv_unpack2(R, p.sig + 4 * ii);
   }
   bool ok = true;
+#ifdef SV_QPROF_NODEC
+  if (dec_wave && false) {
+#else
   if (dec_wave) {
+#endif
 #else
   uint32_t A[8], S[8], hram[16], R[8];
   sv_load_and_hash<MODE>(p, ii, A, S, hram);
@@ -706,7 +719,11 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     sc_reduce512(h, hram);
     sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
   }
+#ifdef SV_QPROF_NOMUL
+  const int W = 0;
+#else
   const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
+#endif
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
   __syncthreads();  // tables visible to the whole quad
@@ -721,6 +738,30 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
   SV_UNROLL for (int k = 0; k < 8; ++k) dg[k] = half ? D.dR[k] : D.dA[k];
   const bool top8 = half ? D.top8R : D.top8A;
   const bool flip = half && D.rneg;
+#if SV_LAT_OWN
+  // own form (quad.h): lane r holds coordinate r of P until the end
+  fe h;
+  qo_identity(h, q);
+  SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
+    int32_t d = sc_pop_top(dg, 4);
+    if (w == W - 1 && top8) d = 8;
+    if (flip) d = -d;
+    int32_t dB0, dB1;
+    fe b;
+    const bool bwin = sv_lat_bdigits(D, w, dB0, dB1);
+    const int32_t dB = half ? dB1 : dB0;
+    if (bwin) qo_load_affine(b, btab + (dB < 0 ? -dB : dB) * SV_BTAB_QUADS, role, dB < 0);  // lands during the doublings
+    if (w != W - 1) {
+      SV_NOUNROLL for (int k = 0; k < 4; ++k) qo_dbl(h, q);
+    }
+    fe m;
+    qo_load_cached(m, tab + (d < 0 ? -d : d) * SV_QENT_DW, role, d < 0);
+    qo_add(h, m, q, d < 0);
+    if (bwin) qo_add(h, b, q, dB < 0);
+  }
+  ge_p3 P;
+  qo_expand(P, h);
+#else
   ge_p3 P;
   fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
   SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
@@ -742,6 +783,7 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     qd_add(P, m, q, d < 0, bwin || w == 0);
     if (bwin) qd_add(P, b, q, dB < 0, w == 0);
   }
+#endif
   // quad 0: P_A + P_R, P_R in cached form from quad 1
   {
     ge_p3 PR;
