@@ -141,7 +141,9 @@ def _check(rc: int) -> None:
 
 
 def _ptr(a: np.ndarray) -> ctypes.c_void_p:
-    return ctypes.c_void_p(a.ctypes.data)
+    # (__array_interface__ is several times cheaper than a.ctypes.data: the
+    # 1k-batch latency path pays this per array)
+    return ctypes.c_void_p(a.__array_interface__["data"][0])
 
 
 # sv_opts.flags kernel-path requests (include/stellar_sigverify.h)

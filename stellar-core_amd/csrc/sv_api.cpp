@@ -33,6 +33,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -494,6 +495,13 @@ void pack(const HostIn& in, size_t lo, size_t m, const Image& im, uint8_t* h) {
   });
 }
 
+// SV_STAGE_TRACE: per-call host staging timings to stderr (developer knob)
+bool stage_trace() {
+  static const bool t = getenv("SV_STAGE_TRACE") != nullptr;
+  return t;
+}
+thread_local double g_trace_pack_us = 0;
+
 // Collects a finished chunk's results from its pinned slot.
 int drain_stage(Stage& s, uint8_t* verdict, uint8_t* keys) {
   if (!s.busy) return SV_OK;
@@ -548,7 +556,9 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
       return rc;
     if (verdict && (rc = s.d_verdict.ensure(m))) return rc;
     if (keys && (rc = s.d_keys.ensure(32 * m))) return rc;
+    const auto t_pack = stage_trace() ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
     pack(in, lo, m, im, (uint8_t*)s.h_in.p);
+    if (stage_trace()) g_trace_pack_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_pack).count();
     SV_HIP(hipMemcpyAsync(s.d_in.p, s.h_in.p, im.bytes, hipMemcpyHostToDevice, up_s));
     if (!single) {
       SV_HIP(hipEventRecord(s.up, D.h2d));
@@ -604,7 +614,12 @@ int host_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t*
   SV_HIP(hipSetDevice(D.phys));
   int rc;
   if ((rc = ready_locked(D))) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  g_trace_pack_us = 0;
   rc = host_slice_locked(D, in, n, verdict, keys, path, keys_cb, cb_ctx, cb_done);
+  if (stage_trace())
+    fprintf(stderr, "SV_STAGE_TRACE n=%zu pack %.1f us total %.1f us\n", n, g_trace_pack_us,
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
   if (rc != SV_OK) {
     // leave the slot reusable: nothing of this call may still be in flight
     (void)hipStreamSynchronize(D.h2d);
