@@ -624,6 +624,14 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
 #ifndef SV_LAT_OWN
 #define SV_LAT_OWN 1
 #endif
+// 1: the base-point part [s]B of (*) (lattice.h) runs on wave 1 after its
+// table build (its own 112 doublings, 8 additions per half) while wave 0
+// runs the -A / -R chains without the 8 base additions per half; wave 0 adds
+// the result at the end (second LDS handoff).  Needs SV_LAT_SPLIT and
+// SV_LAT_OWN.
+#ifndef SV_LAT_BOFF
+#define SV_LAT_BOFF 1
+#endif
 #define SV_OCTET_BLOCK (SV_LAT_SPLIT ? 128 : 64)
 
 template <int MODE>
@@ -706,8 +714,49 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     }
   }
 #if SV_LAT_SPLIT
+#if SV_LAT_BOFF
+  __shared__ int32_t s_bd[SV_OSIGS][2][SV_LB_DIGITS];  // base-point digits (wave 0 -> 1)
+  __shared__ uint32_t s_pb[SV_OSIGS][SV_QENT_DW];       // [s]B, cached form (wave 1 -> 0)
+#endif
   if (dec_wave) {
-    __syncthreads();  // tables and s_dok written
+    __syncthreads();  // tables and s_dok written; s_bd read below
+#if SV_LAT_BOFF
+    {
+      // quad 0: [s_lo] B from e B, quad 1: [s_hi] 2^128 B from e 2^128 B;
+      // digit j carries weight 2^(16 j) (Horner: 16 doublings between digits)
+      int32_t bd[SV_LB_DIGITS];
+      SV_UNROLL for (int j = 0; j < SV_LB_DIGITS; ++j) bd[j] = s_bd[sl][half][j];
+      const sv_u4* btab = p.btab + (half ? SV_LBTAB_ENTRIES * SV_BTAB_QUADS : 0);
+      fe h;
+      qo_identity(h, q);
+      SV_NOUNROLL for (int j = SV_LB_DIGITS - 1; j >= 0; --j) {
+        int32_t dB = bd[SV_LB_DIGITS - 1];
+        SV_UNROLL for (int k = SV_LB_DIGITS - 1; k > 0; --k) bd[k] = bd[k - 1];
+        fe b;
+        qo_load_affine(b, btab + (dB < 0 ? -dB : dB) * SV_BTAB_QUADS, role, dB < 0);  // lands during the doublings
+        if (j != SV_LB_DIGITS - 1) {
+          SV_NOUNROLL for (int k = 0; k < 4 * SV_LB_WIN; ++k) qo_dbl(h, q);
+        }
+        qo_add(h, b, q, dB < 0);
+      }
+      ge_p3 PB;
+      qo_expand(PB, h);
+      // quad 0: + quad 1's half (lanes + 4), then the sum in cached form
+      ge_p3 P1;
+      fe_from_hi(P1.X, PB.X);
+      fe_from_hi(P1.Y, PB.Y);
+      fe_from_hi(P1.Z, PB.Z);
+      fe_from_hi(P1.T, PB.T);
+      ge_cached c1;
+      ge_p3_to_cached(c1, P1);
+      fe mine;
+      fe_pick4(mine, q, c1.T2d, c1.Z, c1.YpX, c1.YmX);  // qd_add's operand order
+      qd_add(PB, mine, q, false, true);
+      ge_p3_to_cached(c1, PB);
+      if (half == 0 && role == 0) sv_store_lentry((sv_u4*)&s_pb[sl][0], c1);
+    }
+    __syncthreads();  // s_pb written
+#endif
     return;
   }
   ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
@@ -726,6 +775,11 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
 #endif
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
+#if SV_LAT_SPLIT && SV_LAT_BOFF
+  if (role == 0) {
+    SV_UNROLL for (int j = 0; j < SV_LB_DIGITS; ++j) s_bd[sl][half][j] = half ? D.dB1[j] : D.dB0[j];
+  }
+#endif
   __syncthreads();  // tables visible to the whole quad
 #if SV_LAT_SPLIT
   ok = ok && s_dok[sl] != 0;
@@ -746,11 +800,17 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     int32_t d = sc_pop_top(dg, 4);
     if (w == W - 1 && top8) d = 8;
     if (flip) d = -d;
+#if SV_LAT_SPLIT && SV_LAT_BOFF
+    const bool bwin = false;  // (the base part runs on wave 1)
+    const int32_t dB = 0;
+    fe b;
+#else
     int32_t dB0, dB1;
     fe b;
     const bool bwin = sv_lat_bdigits(D, w, dB0, dB1);
     const int32_t dB = half ? dB1 : dB0;
     if (bwin) qo_load_affine(b, btab + (dB < 0 ? -dB : dB) * SV_BTAB_QUADS, role, dB < 0);  // lands during the doublings
+#endif
     if (w != W - 1) {
       SV_NOUNROLL for (int k = 0; k < 4; ++k) qo_dbl(h, q);
     }
@@ -797,7 +857,14 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     fe_add(ypx, PR.Y, PR.X);
     fe_sub(ymx, PR.Y, PR.X);
     fe_pick4(mine, q, t2d, PR.Z, ypx, ymx);  // role 0 2dT, 1 Z, 2 Y+X, 3 Y-X (qd_add's operand order)
+#if SV_LAT_SPLIT && SV_LAT_BOFF
+    qd_add(P, mine, q, false, true);
+    __syncthreads();  // [s]B from wave 1
+    qd_load_cached(mine, &s_pb[sl][0], role, false);
     qd_add(P, mine, q, false, false);
+#else
+    qd_add(P, mine, q, false, false);
+#endif
   }
   ok = ok && sv_is_identity(P);
   const bool owner = half == 0 && role == 0;
