@@ -591,6 +591,8 @@ __global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
     uint16_t m16 = 0;
     SV_UNROLL for (int k = 0; k < SV_QSIGS; ++k) m16 |= (uint16_t)(((bal >> (4 * k)) & 1u) << k);
     ((uint16_t*)p.bitmap)[blockIdx.x] = m16;
+    if (blockIdx.x == gridDim.x - 1)  // (bits past n read as 0, as on the throughput path)
+      for (uint32_t b = blockIdx.x + 1; b % 4 != 0; ++b) ((uint16_t*)p.bitmap)[b] = 0;
   }
 }
 
@@ -874,6 +876,10 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     uint8_t m8 = 0;
     SV_UNROLL for (int k = 0; k < SV_OSIGS; ++k) m8 |= (uint8_t)(((bal >> (8 * k)) & 1u) << k);
     ((uint8_t*)p.bitmap)[blockIdx.x] = m8;
+    // the last workgroup clears the rest of the final 64-bit word, as the
+    // throughput path's whole-word ballots do (bits past n read as 0)
+    if (blockIdx.x == gridDim.x - 1)
+      for (uint32_t b = blockIdx.x + 1; b % 8 != 0; ++b) ((uint8_t*)p.bitmap)[b] = 0;
   }
 }
 

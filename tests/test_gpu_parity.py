@@ -125,7 +125,7 @@ def test_device_api_ragged_sizes_and_bitmap(sv, dev, oracle, n, kpath):
     sig[bad_rows, rng.integers(0, 64, len(bad_rows))] ^= 0x04
     tsig.copy_(torch.from_numpy(sig))
     tv = torch.full((n,), 7, dtype=torch.uint8, device=dev)
-    tb = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    tb = torch.full(((n + 63) // 64,), -1, dtype=torch.int64, device=dev)  # bits past n must come back 0
     st = torch.cuda.current_stream(dev).cuda_stream
     sv.verify_device(0, tpk.data_ptr(), tsig.data_ptr(), tm.data_ptr(), n, tv.data_ptr(), tb.data_ptr(), st)
     torch.cuda.synchronize(dev)
@@ -134,8 +134,8 @@ def test_device_api_ragged_sizes_and_bitmap(sv, dev, oracle, n, kpath):
     want[bad_rows] = 0
     assert (got == want).all()
     words = tb.cpu().numpy().view(np.uint64)
-    bits = np.array([(int(words[i // 64]) >> (i % 64)) & 1 for i in range(n)], np.uint8)
-    assert (bits == want).all()
+    bits = np.array([(int(words[i // 64]) >> (i % 64)) & 1 for i in range(64 * len(words))], np.uint8)
+    assert (bits[:n] == want).all() and not bits[n:].any()
     # a few rows against the oracle directly
     pk = tpk.cpu().numpy()
     for i in list(bad_rows[:3]) + [0, n - 1]:
@@ -184,7 +184,7 @@ def test_full_size_properties_1m(sv, dev, oracle):
     sig = tsig.cpu().numpy()
     sig[bad, 32 + rng.integers(0, 32, len(bad))] ^= 0x01
     tsig.copy_(torch.from_numpy(sig))
-    tb = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    tb = torch.full(((n + 63) // 64,), -1, dtype=torch.int64, device=dev)  # bits past n must come back 0
     sv.verify_device(0, tpk.data_ptr(), tsig.data_ptr(), tm.data_ptr(), n, tv.data_ptr(), tb.data_ptr(), st)
     torch.cuda.synchronize(dev)
     got = tv.cpu().numpy()
