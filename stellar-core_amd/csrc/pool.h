@@ -39,26 +39,29 @@ class Pool {
       for (size_t i = 0; i < k; ++i) fn(i);
       return;
     }
+    // grp lives in this frame: a helper's last touch of it (decrement and
+    // notify) happens under grp.mu, and this call returns only after seeing
+    // left == 0 under grp.mu -- never while a helper may still lock or notify
+    // it (an unlocked decrement let run() return first, and the helper then
+    // locked a dead mutex and slept forever, hanging ~Pool's join at exit)
     struct Group {
-      std::atomic<size_t> left;
+      size_t left;
       std::mutex mu;
       std::condition_variable cv;
     } grp;
-    grp.left.store(k - 1);
+    grp.left = k - 1;
     {
       std::lock_guard<std::mutex> g(mu_);
       for (size_t i = 1; i < k; ++i)
         q_.emplace_back([&grp, &fn, i] {
           fn(i);
-          if (grp.left.fetch_sub(1) == 1) {
-            std::lock_guard<std::mutex> gg(grp.mu);
-            grp.cv.notify_all();
-          }
+          std::lock_guard<std::mutex> gg(grp.mu);
+          if (--grp.left == 0) grp.cv.notify_all();
         });
     }
     cv_.notify_all();
     fn(0);
-    while (grp.left.load() != 0) {
+    for (;;) {
       std::function<void()> task;
       {
         std::lock_guard<std::mutex> g(mu_);
@@ -72,7 +75,7 @@ class Pool {
         continue;
       }
       std::unique_lock<std::mutex> lk(grp.mu);
-      grp.cv.wait_for(lk, std::chrono::microseconds(200), [&] { return grp.left.load() == 0; });
+      if (grp.cv.wait_for(lk, std::chrono::microseconds(200), [&] { return grp.left == 0; })) return;
     }
   }
 

@@ -558,7 +558,12 @@ SV_HD void sv_load_lentry(fe& qa, fe& qb, fe& qz, fe& qt, const sv_u4* p, int qs
   }
 }
 
-// {0..8}·P in cached form into tab (9 entries x 10 quads, lane-contiguous)
+// {0..8}·P in cached form into tab (9 entries x 10 quads, lane-contiguous).
+// P comes straight from ge_frombytes, so it is affine (Z = 1): each step adds
+// it with the mixed law (2 Z1 Z2 = 2 Z1, no product; SV_LTAB_MADD).
+#ifndef SV_LTAB_MADD
+#define SV_LTAB_MADD 1
+#endif
 SV_COLD void sv_build_ltab(sv_u4* tab, const ge_p3& P) {
   ge_cached c1, ce;
   ge_p3_to_cached(c1, P);
@@ -568,7 +573,7 @@ SV_COLD void sv_build_ltab(sv_u4* tab, const ge_p3& P) {
   ge_p3 P3 = P;
   ge_p1p1 Q;
   SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
-    ge_add_preswapped(Q, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, false);
+    ge_add_preswapped(Q, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, SV_LTAB_MADD != 0);
     ge_p1p1_to_p3(P3, Q);
     ge_p3_to_cached(ce, P3);
     sv_store_lentry(tab + e * SV_LTAB_QUADS, ce);

@@ -9,13 +9,18 @@ library is loaded so the process holds ONE HIP runtime (torch ships its own
 libamdhip64 with the same soname).
 """
 import ctypes
+import faulthandler
 import importlib
 import os
+import signal
 import subprocess
 import sys
 
 import numpy as np
 import pytest
+
+# SIGUSR1 dumps every thread's Python stack (diagnosing a run that does not exit)
+faulthandler.register(signal.SIGUSR1, all_threads=True)
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(REPO, "tests", "golden")

@@ -45,7 +45,12 @@ def _rank_main(rank, world, port, rows, q):
     full = sh.gather_verdicts(np.array(local, np.uint8), n, world, rank)
     if rank == 0:
         q.put((full.tolist(), sh.verdict_digest(full)))
+        q.close()
+        q.join_thread()  # the result is in the pipe before this process goes
     dist.destroy_process_group()
+    # leave without the interpreter's exit handlers: a library destructor that
+    # stalls at exit must not leave the parent (pytest) waiting on this child
+    os._exit(0)
 
 
 def test_shard_bounds_partition():
@@ -68,11 +73,19 @@ def test_gloo_world2_gather_matches_single_process(world):
     port = _free_port()
     procs = [ctx.Process(target=_rank_main, args=(r, world, port, rows, q)) for r in range(world)]
     for p in procs:
+        p.daemon = True  # never joined at interpreter exit
         p.start()
-    full, digest = q.get(timeout=240)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    try:
+        full, digest = q.get(timeout=240)
+        for p in procs:
+            p.join(timeout=60)
+        codes = [p.exitcode for p in procs]
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(5)
+    assert codes == [0] * world, codes
     sh = importlib.import_module("stellar-core_amd.sharding")
     want = d["verdict"][rows]
     assert np.array_equal(np.array(full, np.uint8), want)
