@@ -190,15 +190,18 @@ def config1(sv, sodium, spath, pk_h, sig_h, msgs, threads, device):
     return out
 
 
-def config5(sv, torch, dev, stream, device, d_pk, d_sig, d_msg, n, tiles=64):
-    """BASELINE config 5 (catchup scale) on one GPU: 64 x 2^20 signatures in ONE
-    device batch -- the libsodium-pinned 2^20 dataset tiled 64x in HBM (every
-    signature is verified in full; the engine has no cache).  Reports the
-    device-API rate (HIP-event kernel time and wall time incl. sync)."""
-    N = n * tiles
-    bpk = d_pk.view(n, 32).repeat(tiles, 1)
-    bsig = d_sig.view(n, 64).repeat(tiles, 1)
-    bmsg = d_msg.view(n, 32).repeat(tiles, 1)
+def config5(sv, torch, dev, stream, device, d_pk, d_sig, d_msg, n, world, rank, barrier, dist, tiles=64):
+    """BASELINE config 5 (catchup scale): 64 x 2^20 signatures sharded as
+    contiguous slices over the job's ranks (one GPU each; 1/2/4/8 GPUs as the
+    driver launches bench.py), each rank verifying its 64/N tiles of its own
+    libsodium-pinned 2^20 dataset in ONE device batch (every signature is
+    verified in full: the engine has no cache).  Barrier-bracketed, max over
+    ranks; a gathered digest of the per-rank verdict digests."""
+    per = tiles // world if tiles % world == 0 else max(1, tiles // world)
+    N = n * per
+    bpk = d_pk.view(n, 32).repeat(per, 1)
+    bsig = d_sig.view(n, 64).repeat(per, 1)
+    bmsg = d_msg.view(n, 32).repeat(per, 1)
     out = torch.zeros(N, dtype=torch.uint8, device=dev)
     bm = torch.zeros((N + 63) // 64, dtype=torch.int64, device=dev)
     sv.verify_device(device, bpk.data_ptr(), bsig.data_ptr(), bmsg.data_ptr(), N, out.data_ptr(), bm.data_ptr(),
@@ -210,21 +213,38 @@ def config5(sv, torch, dev, stream, device, d_pk, d_sig, d_msg, n, tiles=64):
     for _ in range(2):
         out.zero_()
         torch.cuda.synchronize(dev)
+        barrier()
         t0 = time.perf_counter()
         sv.verify_device(device, bpk.data_ptr(), bsig.data_ptr(), bmsg.data_ptr(), N, out.data_ptr(),
                          bm.data_ptr(), stream)
         torch.cuda.synchronize(dev)
+        barrier()
         walls.append(time.perf_counter() - t0)
     sv.timing_enable(False)
     ms, _, sigs = sv.kernel_time(device)
     ok = bool(out.all().item()) and bool((bm == -1).all().item())
+    bits = bm.cpu()
+    wall = min(walls)
+    if world > 1:
+        t = torch.tensor([wall, 0.0 if ok else 1.0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, ok = float(t[0]), float(t[1]) == 0.0
+        parts = [torch.zeros_like(bits) for _ in range(world)]
+        dist.all_gather(parts, bits)  # (equal slices: 64 % world == 0)
+        bits = torch.cat(parts)
+    # the whole batch's verdict bitmap, gathered in global row order
+    digest = hashlib.sha256(bits.numpy().tobytes()).hexdigest()
     del bpk, bsig, bmsg, out, bm
     torch.cuda.empty_cache()
-    return {"signatures": N, "construction": "the libsodium-pinned 2^20 bench dataset tiled %dx in HBM, one "
-                                             "sv_ed25519_verify_device call" % tiles,
-            "device_api_verifies_per_s": N / min(walls), "seconds_per_batch": min(walls),
-            "kernel_verifies_per_s": sigs / (ms * 1e-3) if ms > 0 else None,
-            "all_valid_and_bitmap_full": ok}
+    total = N * world
+    return {"signatures": total, "n_gpus": world, "signatures_per_gpu": N,
+            "construction": "each rank's libsodium-pinned 2^20 bench slice tiled %dx in HBM, one "
+                            "sv_ed25519_verify_device call per rank (contiguous global slices)" % per,
+            "verifies_per_s": total / wall, "seconds_per_batch": wall,
+            "rank0_kernel_verifies_per_s": sigs / (ms * 1e-3) if ms > 0 else None,
+            "all_valid_and_bitmap_full": ok,
+            "gathered_bitmap_sha256": digest,
+            "expected_bitmap_sha256": hashlib.sha256(b"\xff" * (total // 8)).hexdigest()}
 
 
 def config3(n_tx=5000):
@@ -547,10 +567,13 @@ def main():
             t_c1 = time.perf_counter()
             result["config1"] = config1(sv, sodium, spath, pk_h, sig_h, msgs, threads, local)
             log("config 1 (both shapes) in %.1fs" % (time.perf_counter() - t_c1))
-    if rank == 0 and world == 1 and not args.no_config35 and n == 1 << 20:
+    if not args.no_config35 and n == 1 << 20 and 64 % world == 0:
         t_c = time.perf_counter()
-        result["config5"] = config5(sv, torch, dev, stream, local, d_pk, d_sig, d_msg, n)
-        log("config 5 (64M signatures) in %.1fs" % (time.perf_counter() - t_c))
+        c5 = config5(sv, torch, dev, stream, local, d_pk, d_sig, d_msg, n, world, rank, barrier, dist)
+        if rank == 0:
+            result["config5"] = c5
+            log("config 5 (64M signatures on %d GPU(s)) in %.1fs" % (world, time.perf_counter() - t_c))
+    if rank == 0 and world == 1 and not args.no_config35 and n == 1 << 20:
         t_c = time.perf_counter()
         result["config3"] = config3()
         log("config 3 (5000-tx set) in %.1fs" % (time.perf_counter() - t_c))
