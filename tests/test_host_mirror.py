@@ -11,6 +11,7 @@ import ctypes
 import hashlib
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -634,3 +635,45 @@ def test_gpu_config3_full_5000_tx(host, sv, oracle):
         assert pairs > 25000  # (~5.8 signatures per tx on average)
     assert 0 < want_ok.sum() < len(txs)
     host.svh_cache_clear()
+
+
+_POOL_STRESS = r"""
+import ctypes, sys
+import numpy as np
+host = ctypes.CDLL(sys.argv[1])
+stub = ctypes.CDLL(sys.argv[2])
+host.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+host.svh_set_keyed_threshold.argtypes = [ctypes.c_size_t]
+host.svh_set_test_verifier(ctypes.cast(stub.hc_stub_verify, ctypes.c_void_p))
+host.svh_set_keyed_threshold(1 << 30)  # host-hashed: BLAKE2b keys over the helper pool
+n = 1024
+rng = np.random.default_rng(1)
+pk = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+sig = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+msg = rng.integers(0, 256, 32 * n, dtype=np.uint8)
+off = (np.arange(n, dtype=np.uint64) * 32)
+ln = np.full(n, 32, np.uint32)
+out = np.zeros(n, np.uint8)
+for it in range(8000):
+    host.svh_cache_clear()
+    sig[:, 0] = it & 255
+    sig[:, 1] = it >> 8
+    rc = host.svh_verify_sig_batch(pk.ctypes.data_as(ctypes.c_void_p), sig.ctypes.data_as(ctypes.c_void_p), None,
+                                   msg.ctypes.data_as(ctypes.c_void_p), off.ctypes.data_as(ctypes.c_void_p),
+                                   ln.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n),
+                                   out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0 and out.all(), (it, rc)
+print("ok")
+"""
+
+
+def test_helper_pool_many_runs_then_exit(host):
+    """Regression: 8000 host-hashed batches, each fanned out over the helper
+    pool (sv::Pool::run), then a normal interpreter exit.  A helper must never
+    touch the caller's stack group after run() returned (pool.h): the old
+    unlocked decrement left a helper asleep on a dead mutex and the process
+    never exited (static ~Pool joins its threads)."""
+    stub = os.path.join(REPO, "tests", "native", "libhostcore.so")
+    r = subprocess.run([sys.executable, "-c", _POOL_STRESS, host._name, stub], stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=90)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:]
