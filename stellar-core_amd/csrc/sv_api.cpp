@@ -201,16 +201,19 @@ size_t stage_chunk() {
   static const size_t c = std::max<size_t>(1024, env_size("SV_STAGE_CHUNK", (size_t)1 << 18));
   return c;
 }
-// Pipeline fill: the first chunks of a multi-chunk batch are chunk/4 and
-// chunk/2, so the first kernel starts after packing and copying a quarter
-// chunk instead of a whole one (SV_STAGE_RAMP=0: equal chunks).
-bool stage_ramp() {
-  static const bool r = env_size("SV_STAGE_RAMP", 1) != 0;
+// Pipeline fill: the first R chunks of a multi-chunk batch grow geometrically
+// (chunk / 2^R, ..., chunk / 2), so the first kernel starts after packing and
+// copying a small chunk instead of a whole one.  SV_STAGE_RAMP = R (default
+// 2: chunk/4 then chunk/2; 0: equal chunks).
+size_t stage_ramp_steps() {
+  static const size_t r = std::min<size_t>(env_size("SV_STAGE_RAMP", 2), 8);
   return r;
 }
+bool stage_ramp() { return stage_ramp_steps() != 0; }
 size_t chunk_len(size_t c, size_t chunk, size_t left) {
   size_t m = chunk;
-  if (stage_ramp() && c < 2) m = std::max<size_t>(1024, chunk >> (2 - c));
+  const size_t r = stage_ramp_steps();
+  if (c < r) m = std::max<size_t>(1024, chunk >> (r - c));
   return std::min(m, left);
 }
 

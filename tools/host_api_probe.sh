@@ -1,7 +1,7 @@
 set -e
-mkdir -p gpurun_out
+# staging ramp depth and chunk size vs the host-API rate at 2^20 (developer tool)
+mkdir -p gpurun_out/ramp
 P="timeout -k 10 120 python -u tools/host_api_probe.py"
-SV_STAGE_RAMP=0 $P > gpurun_out/probe_r0.json 2>/dev/null
-SV_STAGE_RAMP=1 $P > gpurun_out/probe_r1.json 2>/dev/null
-SV_STAGE_RAMP=1 SV_STAGE_CHUNK=131072 $P > gpurun_out/probe_r1c17.json 2>/dev/null
-SV_STAGE_RAMP=1 SV_HOST_THREADS=15 $P > gpurun_out/probe_r1t15.json 2>/dev/null
+for r in 0 2 3 4 5; do SV_STAGE_RAMP=$r $P > gpurun_out/ramp/r$r.json 2>/dev/null; done
+SV_STAGE_RAMP=4 SV_STAGE_CHUNK=131072 $P > gpurun_out/ramp/r4c17.json 2>/dev/null
+SV_STAGE_RAMP=2 $P > gpurun_out/ramp/r2b.json 2>/dev/null
