@@ -634,6 +634,9 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
 #ifndef SV_LAT_BOFF
 #define SV_LAT_BOFF 1
 #endif
+// (in effect only with both prerequisites; the old-form loop keeps its base
+// additions, so the base part is never added twice)
+#define SV_LAT_BOFF_ON (SV_LAT_BOFF && SV_LAT_SPLIT && SV_LAT_OWN)
 #define SV_OCTET_BLOCK (SV_LAT_SPLIT ? 128 : 64)
 
 template <int MODE>
@@ -716,13 +719,13 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     }
   }
 #if SV_LAT_SPLIT
-#if SV_LAT_BOFF
+#if SV_LAT_BOFF_ON
   __shared__ int32_t s_bd[SV_OSIGS][2][SV_LB_DIGITS];  // base-point digits (wave 0 -> 1)
   __shared__ uint32_t s_pb[SV_OSIGS][SV_QENT_DW];       // [s]B, cached form (wave 1 -> 0)
 #endif
   if (dec_wave) {
     __syncthreads();  // tables and s_dok written; s_bd read below
-#if SV_LAT_BOFF
+#if SV_LAT_BOFF_ON
     {
       // quad 0: [s_lo] B from e B, quad 1: [s_hi] 2^128 B from e 2^128 B;
       // digit j carries weight 2^(16 j) (Horner: 16 doublings between digits)
@@ -777,7 +780,7 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
 #endif
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
-#if SV_LAT_SPLIT && SV_LAT_BOFF
+#if SV_LAT_BOFF_ON
   if (role == 0) {
     SV_UNROLL for (int j = 0; j < SV_LB_DIGITS; ++j) s_bd[sl][half][j] = half ? D.dB1[j] : D.dB0[j];
   }
@@ -802,7 +805,7 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     int32_t d = sc_pop_top(dg, 4);
     if (w == W - 1 && top8) d = 8;
     if (flip) d = -d;
-#if SV_LAT_SPLIT && SV_LAT_BOFF
+#if SV_LAT_BOFF_ON
     const bool bwin = false;  // (the base part runs on wave 1)
     const int32_t dB = 0;
     fe b;
@@ -859,7 +862,7 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     fe_add(ypx, PR.Y, PR.X);
     fe_sub(ymx, PR.Y, PR.X);
     fe_pick4(mine, q, t2d, PR.Z, ypx, ymx);  // role 0 2dT, 1 Z, 2 Y+X, 3 Y-X (qd_add's operand order)
-#if SV_LAT_SPLIT && SV_LAT_BOFF
+#if SV_LAT_BOFF_ON
     qd_add(P, mine, q, false, true);
     __syncthreads();  // [s]B from wave 1
     qd_load_cached(mine, &s_pb[sl][0], role, false);
