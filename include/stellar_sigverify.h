@@ -158,7 +158,8 @@ int sv_ed25519_verify_batch_fixed(const uint8_t* pk, const uint8_t* sig, const u
  * If fixed_msg_len != 0, message i = d_msg[i*fixed_msg_len ..] and
  * d_msg_off/d_msg_len are ignored (may be NULL).  d_bitmap (optional, may be
  * NULL) receives one bit per signature, 64 per word, bit (i % 64) of word
- * i / 64 (wave-level ballot compaction of the verdicts).
+ * i / 64 (wave-level ballot compaction of the verdicts); it must hold
+ * ceil(n / 64) words, and the bits past n in the last word are written 0.
  * `stream` is a hipStream_t (NULL = legacy default stream): the work is
  * ordered after prior work on `stream` and later work on `stream` is ordered
  * after it; the call itself does not block.
