@@ -115,7 +115,7 @@ def test_fixed_256_reference_bench_shape(sv, dev, golden, oracle, kpath):
     assert (out == want).all() and want.sum() == len(rows) // 2
 
 
-@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000, 4097])
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 63, 64, 65, 255, 256, 257, 1000, 4097, 12288, 12289])
 def test_device_api_ragged_sizes_and_bitmap(sv, dev, oracle, n, kpath):
     seeds, msgs = _seed_msg(10_000, 10_000 + n)
     tpk, tsig, tm = _gpu_sign(sv, dev, seeds, msgs)
