@@ -665,6 +665,13 @@ SV_HD void fe_const_2d(fe& h) {
                           0x0f3d130, 0x3407977, 0x19ce331, 0x1c56dff, 0x0901b67};
   SV_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = c[i];
 }
+// 1/d (the main kernel's first window builds P = 2 Q from a cached entry:
+// 2T = (2dT) / d)
+SV_HD void fe_const_dinv(fe& h) {
+  const uint32_t c[10] = {0x1c9f843, 0x03c9db3, 0x285c4bc, 0x0c213ca, 0x02d775a,
+                          0x1b9cf66, 0x3108a66, 0x1c86562, 0x1214d5c, 0x10241fb};
+  SV_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = c[i];
+}
 SV_HD void fe_const_sqrtm1(fe& h) {
   const uint32_t c[10] = {0x20ea0b0, 0x186c9d2, 0x08f189d, 0x035697f, 0x0bd0c60,
                           0x1fbd7a7, 0x2804c9e, 0x1e16569, 0x004fc1d, 0x0ae0c92};

@@ -350,6 +350,9 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   SV_PHASE(4);
 }
 
+#ifndef SV_MAIN_TOPINIT
+#define SV_MAIN_TOPINIT 1
+#endif
 // The main kernel's scalar multiplication: the step machine of
 // sv_lat_scalarmult (verify_core.h, STAGED with one stage region) with the
 // digits streamed from the signature's record instead of held in registers
@@ -368,9 +371,45 @@ __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw,
   const bool rneg = (flags & SV_REC_RNEG) != 0;
   // current and next digit words (the word changes every 8 windows)
   uint32_t curA = rw[7], curR = rw[15], nxtA = rw[6], nxtR = rw[14];
-  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
   ge_p1p1 Q;
+#if SV_MAIN_TOPINIT
+  {
+    // Window W-1 (no doublings; above every base-point window), peeled: P is
+    // the identity, so P + Q_A = Q_A is taken straight from the (pre-swapped)
+    // cached entry as (2X : 2Y : 2Z : 2T) -- (Y+X) - (Y-X), (Y+X) + (Y-X), 2Z
+    // and 2T = (2dT) / d, negated for a negative digit -- instead of a full
+    // addition and conversion (8 products -> 1); then the R entry is added.
+    int32_t dA = top8A ? 8 : sv_nibble(curA, 63), dR = top8R ? 8 : sv_nibble(curR, 63);
+    if (rneg) dR = -dR;
+    fe qa, qb, qz, qt;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sv_stage_lentry(stage, tabA + (dA < 0 ? -dA : dA) * SV_LTAB_QUADS);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sv_load_lentry(qa, qb, qz, qt, stage + __lane_id(), 64, dA < 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sv_stage_lentry(stage, tabR + (dR < 0 ? -dR : dR) * SV_LTAB_QUADS);
+    fe_sub(P.X, qa, qb);
+    fe_add(P.Y, qa, qb);
+    fe_add(P.Z, qz, qz);
+    fe di, nt;
+    fe_const_dinv(di);
+    fe_mul(P.T, qt, di);
+    fe_neg(nt, P.T);
+    SV_UNROLL for (int i = 0; i < 10; ++i) P.T.v[i] = dA < 0 ? nt.v[i] : P.T.v[i];
+    fe_weak(P.X);  // (the addition below takes p at R)
+    fe_weak(P.Y);
+    fe_weak(P.Z);
+    fe_weak(P.T);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sv_load_lentry(qa, qb, qz, qt, stage + __lane_id(), 64, dR < 0);
+    ge_add_preswapped(Q, P, qa, qb, qz, qt, dR < 0, false);
+    ge_p1p1_to_p3_opt(P, Q, false);  // (a doubling comes next)
+  }
+  SV_NOUNROLL for (int w = W - 2; w >= 0; --w) {
+#else
+  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
   SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
+#endif
     const int pos = w + 64 - W;  // (wave-uniform)
     if ((pos & 7) == 7 && w != W - 1) {
       curA = nxtA;
