@@ -9,6 +9,7 @@
 #include <cstddef>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -39,24 +40,27 @@ class Pool {
       for (size_t i = 0; i < k; ++i) fn(i);
       return;
     }
-    // grp lives in this frame: a helper's last touch of it (decrement and
-    // notify) happens under grp.mu, and this call returns only after seeing
-    // left == 0 under grp.mu -- never while a helper may still lock or notify
-    // it (an unlocked decrement let run() return first, and the helper then
-    // locked a dead mutex and slept forever, hanging ~Pool's join at exit)
+    // The group is shared with the helpers (heap, reference-counted): a
+    // helper's last touch of it -- decrement and notify under grp->mu --
+    // can never reach memory this call has already released, and run()
+    // returns only after seeing zero under grp->mu, i.e. after every fn(i).
+    // (An earlier stack-allocated group let run() return while a helper was
+    // still to lock its mutex; the helper then slept forever on dead stack
+    // memory and ~Pool's join hung process exit.)
     struct Group {
       size_t left;
       std::mutex mu;
       std::condition_variable cv;
-    } grp;
-    grp.left = k - 1;
+    };
+    auto grp = std::make_shared<Group>();
+    grp->left = k - 1;
     {
       std::lock_guard<std::mutex> g(mu_);
       for (size_t i = 1; i < k; ++i)
-        q_.emplace_back([&grp, &fn, i] {
+        q_.emplace_back([grp, &fn, i] {
           fn(i);
-          std::lock_guard<std::mutex> gg(grp.mu);
-          if (--grp.left == 0) grp.cv.notify_all();
+          std::lock_guard<std::mutex> gg(grp->mu);
+          if (--grp->left == 0) grp->cv.notify_all();
         });
     }
     cv_.notify_all();
@@ -74,8 +78,13 @@ class Pool {
         task();
         continue;
       }
-      std::unique_lock<std::mutex> lk(grp.mu);
-      if (grp.cv.wait_for(lk, std::chrono::microseconds(200), [&] { return grp.left == 0; })) return;
+      // (a bounded wait, so tasks queued meanwhile -- nested run() calls --
+      // are picked up; system_clock: libstdc++ then uses the timed wait that
+      // ThreadSanitizer models, tests of this pool run under it clean)
+      std::unique_lock<std::mutex> lk(grp->mu);
+      if (grp->cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::microseconds(200),
+                             [&] { return grp->left == 0; }))
+        return;
     }
   }
 
