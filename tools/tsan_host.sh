@@ -20,4 +20,29 @@ print(re.search(r'_POOL_STRESS = r"""(.*?)"""', src, re.S).group(1).replace("ran
 PY
 TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$(gcc -print-file-name=libtsan.so) \
     python3 $O/stress.py $O/libstellar_host.so "$R/tests/native/libhostcore.so" > $O/out.txt 2>&1 || true
-echo "TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out.txt || true); stress: $(tail -1 $O/out.txt)"
+echo "pool stress: TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out.txt || true); result: $(tail -1 $O/out.txt)"
+# the micro-batcher (VerifyMicroBatcher: producer shards, flush workers,
+# futures and fire-and-forget posts) under a native 8-producer flood
+cat > $O/mb.py <<'PY'
+import ctypes, sys
+import numpy as np
+host = ctypes.CDLL(sys.argv[1]); stub = ctypes.CDLL(sys.argv[2])
+host.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+host.svh_set_test_verifier(ctypes.cast(stub.hc_stub_verify, ctypes.c_void_p))
+n = 20000
+rng = np.random.default_rng(2)
+pk = rng.integers(0, 256, (n, 32), dtype=np.uint8); sig = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+msg = rng.integers(0, 256, 32 * n, dtype=np.uint8)
+off = np.arange(n, dtype=np.uint64) * 32; ln = np.full(n, 32, np.uint32); out = np.zeros(n, np.uint8)
+P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+for ff in (0, 1):
+    host.svh_cache_clear()
+    rc = host.svh_mb_run_ex(P(pk), P(sig), P(msg), P(off), P(ln), ctypes.c_size_t(n), 8, 3, ctypes.c_uint32(512),
+                            ctypes.c_uint32(200), ctypes.c_uint32(0), ff, P(out), None)
+    assert rc == 0, rc
+    assert ff or out.all()
+print("ok")
+PY
+TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$(gcc -print-file-name=libtsan.so) \
+    python3 $O/mb.py $O/libstellar_host.so "$R/tests/native/libhostcore.so" > $O/out_mb.txt 2>&1 || true
+echo "micro-batcher flood: TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out_mb.txt || true); result: $(tail -1 $O/out_mb.txt)"
