@@ -249,14 +249,18 @@ __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_lat_ker
 //                   hide their latency); writes the signature's tables and a
 //                   7-quad digit record into the chunk workspace, and each
 //                   wave's window count W into wmax[group].
-//   sv_main_kernel  the hot loop only, 2 waves/SIMD at 256 VGPRs, persistent.
+//   sv_main_kernel  the hot loop only, SV_MAIN_WAVES (3) waves/SIMD, persistent.
+// SV_PREP_WAVES = 3 (168 VGPRs, 128 B of scratch in the table build) measured
+// 1.7-4.2 % faster prep than 2 (199 VGPRs, no scratch) in three A/B runs
+// (profiles/r02/ab_prep_waves*.txt): the extra wave hides more issue latency
+// than the spills cost.
 // Workspace per signature of the chunk: SV_SLOT_QUADS_L quads of tables, then
 // (separate array) SV_REC_QUADS quads of digits/flags.
 #ifndef SV_SPLIT
 #define SV_SPLIT 1
 #endif
 #ifndef SV_PREP_WAVES
-#define SV_PREP_WAVES 2
+#define SV_PREP_WAVES 3
 #endif
 #ifndef SV_CHUNK
 #define SV_CHUNK (1u << 20)
