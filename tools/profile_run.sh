@@ -9,7 +9,7 @@ O=$(realpath -m "${1:-$R/gpurun_out/prof}")
 N=${2:-1048576}
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps 6 --warmup 1 --no-cpu --no-latency --no-host-api --batch $N"
+B="$R/bench.py --steps 6 --warmup 1 --no-cpu --no-latency --no-host-api --no-config1 --no-config35 --batch $N"
 timeout -k 10 300 rocprofv3 --output-format csv --kernel-trace --stats -d "$O/kt" -o kt -- python3 $B > "$O/kt.log" 2>&1
 timeout -k 10 300 rocprofv3 --output-format csv --pmc FETCH_SIZE -d "$O/fetch" -o fetch -- python3 $B > "$O/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --output-format csv --pmc WRITE_SIZE -d "$O/write" -o write -- python3 $B > "$O/write.log" 2>&1
