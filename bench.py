@@ -103,6 +103,45 @@ def cpu_verify_rate(pk, sig, msg, mlen, threads, sodium_path):
     return n / dt, dt, out
 
 
+def host_cpus():
+    """Threads for the CPU baseline: every CPU this process may run on
+    (sched_getaffinity), limited by the cgroup CPU quota when one is set (a
+    quota below the affinity count means only that many run at once)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        quota = None
+    threads = aff if quota is None else max(1, min(aff, int(quota + 1e-9)))
+    threads = min(threads, 256)  # (oracle/cpu_baseline.c thread table)
+    return threads, {"sched_getaffinity": aff, "os_cpu_count": os.cpu_count(), "cgroup_quota_cpus": quota,
+                     "threads_used": threads}
+
+
+def cpu_batch_latency(spath, pk, sig, buf, off, ln, threads, iters):
+    """p50 wall time of one libsodium batch (one crypto_sign_verify_detached per
+    signature on `threads` pthreads, oracle/cpu_baseline.c cpubase_sodium_batch)."""
+    base = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+    base.cpubase_set_sodium.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    if base.cpubase_set_sodium(spath.encode(), threads) != 0:
+        raise RuntimeError("libsodium setup failed")
+    base.cpubase_sodium_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p]
+    out = np.zeros(len(ln), np.uint8)
+    ts = []
+    for _ in range(iters):
+        t1 = time.perf_counter()
+        rc = base.cpubase_sodium_batch(pk.ctypes.data, sig.ctypes.data, buf.ctypes.data, off.ctypes.data,
+                                       ln.ctypes.data, len(ln), out.ctypes.data)
+        ts.append((time.perf_counter() - t1) * 1e3)
+        if rc != 0:
+            raise RuntimeError("cpubase_sodium_batch failed")
+    return float(np.percentile(ts, 50)), out
+
+
 def sodium_path():
     for p in ("/opt/conda/lib/libsodium.so.23", "libsodium.so.23", "libsodium.so"):
         try:
@@ -515,29 +554,65 @@ def main():
         m_off = np.zeros(len(lmsgs), np.uint64)
         m_off[1:] = np.cumsum(m_len[:-1], dtype=np.uint64)
         m_buf = np.frombuffer(b"".join(lmsgs), np.uint8)
-        for _ in range(5):
-            out = sv.verify_batch(pk_a, sg_a, m_buf, m_off, m_len, device=local)
-        lat = []
-        for _ in range(args.latency_iters):
-            t1 = time.perf_counter()
-            out = sv.verify_batch(pk_a, sg_a, m_buf, m_off, m_len, device=local)
-            lat.append((time.perf_counter() - t1) * 1e3)
-        lat = np.array(lat)
+        def timed(iters):
+            lat, outs = [], None
+            for _ in range(iters):
+                t1 = time.perf_counter()
+                outs = sv.verify_batch(pk_a, sg_a, m_buf, m_off, m_len, device=local)
+                lat.append((time.perf_counter() - t1) * 1e3)
+            return np.array(lat), outs
+
+        # steady state of an SCP flood: the validators' key tables are built
+        # (low-priority stream) after the first batch, then every batch runs
+        # the warm-key comb kernel
+        for _ in range(3):
+            sv.verify_batch(pk_a, sg_a, m_buf, m_off, m_len, device=local)
+        sv.key_cache_wait(local)
+        timed(5)
+        st0 = sv.key_cache_stats(local)
+        lat, out = timed(args.latency_iters)
+        st1 = sv.key_cache_stats(local)
+        warm = st1["warm_batches"] - st0["warm_batches"]
+        # cold keys: key cache off (every batch on the octet kernel, no per-key state)
+        cap0 = st1["capacity"]
+        sv.set_key_cache(0)
+        timed(5)
+        lat_c, out_c = timed(args.latency_iters)
+        sv.set_key_cache(cap0)
         result["latency_1k"] = {
             "batch": len(pks),
             "p50_ms": float(np.percentile(lat, 50)),
             "p99_ms": float(np.percentile(lat, 99)),
             "iters": args.latency_iters,
-            "path": "host API sv_ed25519_verify_batch, one call per batch (pack into pinned staging + H2D + "
-                    "kernel + D2H; SV_PATH_AUTO takes the latency kernel at this size)",
+            "key_cache": "warm: %d of %d timed batches ran the comb kernel (100 validator keys cached after the "
+                         "first batch; csrc/comb.h)" % (warm, args.latency_iters),
+            "path": "host API sv_ed25519_verify_batch, one call per batch on the slot's latency lane (pack into "
+                    "pinned staging + H2D + kernel + D2H + sync)",
             "set": src,
             "verdicts_match_libsodium": bool((out == expect).all()),
         }
+        result["latency_1k_cold_keys"] = {
+            "p50_ms": float(np.percentile(lat_c, 50)),
+            "p99_ms": float(np.percentile(lat_c, 99)),
+            "iters": args.latency_iters,
+            "key_cache": "off (sv_set_key_cache(0)): the octet kernel, no per-key state -- what a batch of "
+                         "never-seen keys gets",
+            "verdicts_match_libsodium": bool((out_c == expect).all()),
+        }
+        spath_l = sodium_path() if sodium is not None else None
+        if spath_l is not None and world == 1 and not args.no_cpu:
+            thr, _ = host_cpus()
+            one, o1 = cpu_batch_latency(spath_l, pk_a, sg_a, m_buf, m_off, m_len, 1, 5)
+            allc, o2 = cpu_batch_latency(spath_l, pk_a, sg_a, m_buf, m_off, m_len, thr, 21)
+            result["latency_1k"]["cpu_libsodium"] = {
+                "p50_ms_1thread": one, "p50_ms_all_cores": allc, "threads": thr,
+                "verdicts_match": bool((o1 == expect).all() and (o2 == expect).all()),
+                "what": "the same 1000-signature set, one libsodium crypto_sign_verify_detached per signature "
+                        "(oracle/cpu_baseline.c cpubase_sodium_batch, static partition over pthreads)"}
 
     # ---- CPU baseline (rank 0, N=1 only)
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-        threads = max(1, min(threads, 64))
+        threads, cpu_info = host_cpus()
         spath = sodium_path() if sodium is not None else None
         if spath is not None:
             kind = "reference"
@@ -560,6 +635,7 @@ def main():
             "sample": desc + " (%.2f s wall on %d pthreads, static contiguous partition; native harness "
                              "oracle/cpu_baseline.c)" % (dt, threads),
             "single_thread_value": rate1,
+            "host_cpus": cpu_info,
             "cpu_verdicts_all_valid": bool(out.all() and out1.all()),
             "gpu_over_cpu": value / rate if rate > 0 else None,
         }

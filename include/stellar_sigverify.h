@@ -209,6 +209,30 @@ int sv_verify_cache_keys_device(int device, const void* d_pk, const void* d_sig,
 int sv_sha256_device(int device, const void* d_data, const uint64_t* d_off, const uint32_t* d_len,
                      uint32_t fixed_len, size_t n, void* d_digests, void* stream);
 
+/* ---- Warm-key latency path (csrc/comb.h, csrc/sv_comb.hip) ---------------
+ * Each device slot keeps a bounded cache of per-public-key tables
+ * ({0..8} * 16^j * (-A), 108 KiB per key) in HBM.  A latency-path host batch
+ * whose keys are all cached runs the comb kernel: libsodium's equation
+ * [S]B + [h](-A) == R evaluated as a sum of 96 table entries, no scalar
+ * multiplication.  Any other batch runs the octet kernel, after which its
+ * keys (on their second sighting) are built on a low-priority stream for the
+ * next batch.  Verdicts are identical on both kernels; the cache holds only
+ * data derived from public keys.  Default capacity 1024 keys (or the
+ * SV_KEY_CACHE environment variable); 0 disables the warm path.  Drains and
+ * clears every slot's cache. */
+int sv_set_key_cache(size_t capacity);
+/* Blocks until every key-table build queued on `device` has finished. */
+int sv_key_cache_wait(int device);
+typedef struct sv_key_cache_stats {
+  uint64_t capacity;     /* keys the cache holds at most */
+  uint64_t keys;         /* keys cached or being built */
+  uint64_t warm_batches; /* latency-lane batches served by the comb kernel */
+  uint64_t cold_batches; /* latency-lane batches served by the octet kernel */
+  uint64_t keys_built;   /* key-table builds queued */
+  uint64_t evictions;
+} sv_key_cache_stats;
+int sv_key_cache_get_stats(int device, sv_key_cache_stats* out);
+
 /* Test knobs (0 in production).  TRIVIAL_PAIR: every lane verifies through the
  * fallback pair (h, 1) of the half-size equation (lattice.h), i.e. the
  * full-length scalar; MAX_WINDOWS: every wave runs all 64 windows; FAIL: every

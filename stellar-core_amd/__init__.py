@@ -26,7 +26,7 @@ LIB_PATH = os.path.join(_HERE, "libstellar_sigverify.so")
 
 
 VERIFY_KERNEL_SOURCES = ("sv_common.h", "fe25519.h", "fe_asm_gen.h", "ge25519.h", "sc25519.h", "lattice.h", "sha512_dev.h",
-                         "verify_core.h", "quad.h", "sv_kernels.hip")
+                         "verify_core.h", "quad.h", "sv_kparams.h", "sv_kernels.hip")
 
 # kernel paths (include/stellar_sigverify.h)
 PATH_AUTO, PATH_THROUGHPUT, PATH_LATENCY = 0, 1, 2
@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "sv_verify_cache_keys_device", "sv_sha256_device", "sv_set_kernel_path",
     "sv_ed25519_verify_batch_gather", "sv_ed25519_verify_batch_gather_cb", "sv_ed25519_verify_batch_cpu", "sv_ed25519_verify_cpu",
     "sv_set_device_map", "sv_set_min_shard", "sv_set_debug_flags", "sv_workspace_bytes", "sv_pinned_bytes",
+    "sv_set_key_cache", "sv_key_cache_wait", "sv_key_cache_get_stats",
 )
 
 # test knobs (include/stellar_sigverify.h sv_set_debug_flags)
@@ -77,6 +78,11 @@ class SigVerifyError(RuntimeError):
 class sv_opts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("max_devices", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class KeyCacheStats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in ("capacity", "keys", "warm_batches", "cold_batches", "keys_built",
+                                                "evictions")]
 
 
 _lib: Optional[ctypes.CDLL] = None
@@ -130,6 +136,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sv_set_debug_flags.argtypes = [ctypes.c_uint32]
     lib.sv_workspace_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
     lib.sv_pinned_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
+    lib.sv_set_key_cache.argtypes = [sz]
+    lib.sv_key_cache_wait.argtypes = [ctypes.c_int]
+    lib.sv_key_cache_get_stats.argtypes = [ctypes.c_int, ctypes.POINTER(KeyCacheStats)]
     _lib = lib
     return lib
 
@@ -379,3 +388,19 @@ def kernel_time_reset() -> None:
 
 def synchronize(device: int = 0) -> None:
     _check(load_library().sv_device_synchronize(device))
+
+
+def set_key_cache(capacity: int) -> None:
+    """Key-cache capacity of the warm-key latency path (0: off); clears it."""
+    _check(load_library().sv_set_key_cache(int(capacity)))
+
+
+def key_cache_wait(device: int = 0) -> None:
+    """Blocks until the device's queued key-table builds have finished."""
+    _check(load_library().sv_key_cache_wait(device))
+
+
+def key_cache_stats(device: int = 0) -> dict:
+    st = KeyCacheStats()
+    _check(load_library().sv_key_cache_get_stats(device, ctypes.byref(st)))
+    return {f: int(getattr(st, f)) for f, _ in KeyCacheStats._fields_}

@@ -77,7 +77,11 @@ TxSigResult checkTransactionSignatures(TransactionSigInfo const& tx, AccountSnap
     if (acc) {
       ok = checker.checkSignature(accountSigners(*acc), acc->thresholds[op.level]);
       if (!ok) opc = opBAD_AUTH;
-    } else if (forApply || !op.sourceAccount) {
+    } else if (!op.sourceAccount) {
+      // (processSignatures calls OperationFrame::checkSignature with
+      // forApply = false, TransactionFrame.cpp:1130-1131: a missing op-source
+      // account is checked by its key alone in BOTH modes; only a missing
+      // transaction source gives opNO_ACCOUNT, OperationFrame.cpp:194-198)
       ok = false;
       opc = opNO_ACCOUNT;
     } else {

@@ -99,8 +99,12 @@ struct TxSigResult {
 // forApply = false: the validation path (checkValid: operations fast-fail on
 // the first invalid one).  forApply = true: the apply path
 // (TransactionFrame::apply -> processSignatures, TransactionFrame.cpp:1091-1156:
-// no operation checks before protocol 10, every operation checked, a missing
-// operation source account is opNO_ACCOUNT, OperationFrame.cpp:194-198).
+// no operation checks before protocol 10, then every operation checked, no
+// fast fail).  Both paths check operations with OperationFrame::checkSignature's
+// forApply = false rule (processSignatures passes false, :1130-1131): a missing
+// op-source account named by the operation is checked by its key alone
+// (checkSignatureNoAccount), and only a missing transaction source -- no
+// op source set -- is opNO_ACCOUNT (OperationFrame.cpp:186-207).
 TxSigResult checkTransactionSignatures(TransactionSigInfo const& tx, AccountSnapshot const& accounts,
                                        uint32_t protocol, SignatureBatchPrefetch const* prefetched = nullptr,
                                        bool forApply = false);

@@ -46,6 +46,8 @@
 #include <vector>
 
 #include "../../include/stellar_sigverify.h"
+#include "comb.h"
+#include "keycache.h"
 #include "pool.h"
 
 extern "C" {
@@ -63,6 +65,16 @@ hipError_t sv_launch_sign(unsigned grid, const void* seed, const void* msg, uint
 hipError_t sv_launch_hash(int kind, unsigned max_blocks, const void* pk, const void* sig, const void* msg,
                           const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n, void* out,
                           hipStream_t s);
+// warm-key latency path (sv_comb.hip)
+size_t sv_comb_btab_bytes(void);
+size_t sv_key_slot_bytes(void);
+hipError_t sv_launch_comb_btab(uint32_t* d_ctab, hipStream_t s);
+hipError_t sv_launch_keytab(const void* d_pks, const uint32_t* d_slots, uint32_t nkeys, uint32_t* d_ktab,
+                            uint32_t* d_kstat, hipStream_t s);
+int sv_comb_spw(uint64_t n, int cus);
+hipError_t sv_launch_comb(int mode, int spw, const void* pk, const void* sig, const void* msg, const uint64_t* off,
+                          const uint32_t* len, uint32_t fixed_len, uint64_t n, void* verdict, const uint32_t* kslot,
+                          const uint32_t* ktab, const uint32_t* kstat, const uint32_t* ctab, hipStream_t s);
 }
 
 namespace {
@@ -156,6 +168,44 @@ struct Stage {
   size_t lo = 0, m = 0;
 };
 
+// Latency lane of a slot.  Batches that take the latency kernels (one staging
+// chunk, SV_PATH_LATENCY) run here on their own high-priority stream, pinned
+// staging and mutex, so an SCP batch never waits on the host side for the
+// slot's bulk work (a tx set or a catchup batch holding Device::mu).  The lane
+// also owns the key cache of the warm-key kernel (keycache.h, comb.h): a batch
+// whose keys are all cached runs sv_comb_kernel, any other batch the octet
+// kernel, after which its new keys are queued for a table build on the
+// low-priority build stream.
+struct LatLane {
+  std::mutex mu;
+  bool ready = false;
+  hipStream_t stream = nullptr;  // verify work (highest priority)
+  hipStream_t build = nullptr;   // key-table builds (lowest priority)
+  hipEvent_t ev_lat = nullptr, done = nullptr, keys_down = nullptr;
+  HostBuf h_in, h_out, h_build;
+  DevBuf d_in, d_out, d_keys, d_build;
+  void* ctab = nullptr;  // tables of B (built at lane init)
+  DevBuf ktab, kstat;    // tables of -A per cached key, status per slot
+  size_t cap = 0;        // key-cache capacity the index / tables are sized for
+  sv::KeyIndex index;
+  uint64_t tick = 0, next_gen = 1;
+  struct Build {
+    uint64_t gen;
+    hipEvent_t uploaded, done;
+    std::vector<int32_t> slots;
+  };
+  std::deque<Build> inflight;
+  // kernel-time accounting (sv_timing_enable), as Device::pending
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  std::vector<uint64_t> pending_n;
+  double total_ms = 0;
+  uint64_t launches = 0, sigs = 0;
+  std::vector<uint32_t> kslots;          // per signature of the batch being planned
+  std::vector<const uint8_t*> fresh_pk;  // keys admitted by it
+  std::vector<int32_t> fresh_slot;
+  uint64_t warm = 0, cold = 0, built = 0, evicted = 0;
+};
+
 struct Device {
   int slot = -1;
   int phys = -1;
@@ -175,6 +225,7 @@ struct Device {
   std::vector<uint64_t> pending_n;
   double total_ms = 0;
   uint64_t launches = 0, sigs = 0;
+  LatLane lat;
 };
 
 std::mutex g_mu;
@@ -633,6 +684,337 @@ int host_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t*
   return rc;
 }
 
+// ------------------------------------------------------------ latency lane
+std::atomic<size_t> g_key_cap{~(size_t)0};  // sv_set_key_cache (~0: SV_KEY_CACHE or the default)
+size_t key_cache_cap() {
+  const size_t v = g_key_cap.load();
+  return v != ~(size_t)0 ? v : env_size("SV_KEY_CACHE", 1024);
+}
+// keys admitted for a table build per batch (a flood of fresh keys costs at
+// most this many ~0.3 ms builds on the low-priority stream per batch)
+constexpr size_t kMaxBuildsPerBatch = 256;
+
+void lat_drop_builds(LatLane& L) {
+  for (auto& b : L.inflight) {
+    (void)hipEventDestroy(b.uploaded);
+    (void)hipEventDestroy(b.done);
+  }
+  L.inflight.clear();
+}
+
+// Caller holds L.mu and has set the device.
+void release_lat(LatLane& L) {
+  if (!L.ready) return;
+  (void)hipStreamSynchronize(L.stream);
+  (void)hipStreamSynchronize(L.build);
+  lat_drop_builds(L);
+  for (auto& pr : L.pending) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  L.pending.clear();
+  L.pending_n.clear();
+  L.h_in.release(); L.h_out.release(); L.h_build.release();
+  L.d_in.release(); L.d_out.release(); L.d_keys.release(); L.d_build.release();
+  L.ktab.release(); L.kstat.release();
+  if (L.ctab) (void)hipFree(L.ctab);
+  L.ctab = nullptr;
+  if (L.ev_lat) (void)hipEventDestroy(L.ev_lat);
+  if (L.done) (void)hipEventDestroy(L.done);
+  if (L.keys_down) (void)hipEventDestroy(L.keys_down);
+  L.ev_lat = L.done = L.keys_down = nullptr;
+  if (L.stream) (void)hipStreamDestroy(L.stream);
+  if (L.build) (void)hipStreamDestroy(L.build);
+  L.stream = L.build = nullptr;
+  L.index.reset(0);
+  L.cap = 0;
+  L.ready = false;
+}
+
+// Creates the lane (caller holds D.lat.mu, device set).  Lock order: lat.mu
+// before D.mu (the slot's base-point tables, which the octet kernel reads,
+// are created under D.mu and immutable afterwards).
+int lat_ready(Device& D) {
+  LatLane& L = D.lat;
+  if (L.ready) return SV_OK;
+  int rc;
+  {
+    std::lock_guard<std::mutex> g(D.mu);
+    if ((rc = ready_locked(D))) return rc;
+  }
+  int least = 0, greatest = 0;
+  SV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  SV_HIP(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, greatest));
+  L.ready = true;  // (release_lat cleans up whatever exists from here on)
+  hipError_t e = hipStreamCreateWithPriority(&L.build, hipStreamNonBlocking, least);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&L.ev_lat, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&L.done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&L.keys_down, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc(&L.ctab, sv_comb_btab_bytes());
+  if (e == hipSuccess) e = sv_launch_comb_btab((uint32_t*)L.ctab, L.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(L.stream);
+  if (e != hipSuccess) {
+    release_lat(L);
+    return hip_fail(e, "latency lane init");
+  }
+  const size_t build_bytes = kMaxBuildsPerBatch * 36;
+  if ((rc = L.h_build.ensure(build_bytes)) || (rc = L.d_build.ensure(build_bytes))) {
+    release_lat(L);
+    return rc;
+  }
+  return SV_OK;
+}
+
+// Sizes the key cache to key_cache_cap() (caller holds L.mu, device set).  An
+// allocation failure leaves the cache off: the octet kernel needs no tables.
+void lat_cache_ready(LatLane& L) {
+  const size_t cap = key_cache_cap();
+  if (cap == L.cap) return;
+  (void)hipStreamSynchronize(L.stream);
+  (void)hipStreamSynchronize(L.build);
+  lat_drop_builds(L);
+  L.ktab.release();
+  L.kstat.release();
+  L.index.reset(0);
+  L.cap = 0;
+  if (cap == 0) return;
+  if (L.ktab.ensure(cap * sv_key_slot_bytes()) != SV_OK || L.kstat.ensure(cap * 4) != SV_OK) {
+    L.ktab.release();
+    L.kstat.release();
+    return;
+  }
+  L.index.reset(cap);
+  L.cap = cap;
+}
+
+// Promotes the slots of finished builds to READY.
+void lat_poll(LatLane& L) {
+  while (!L.inflight.empty()) {
+    LatLane::Build& b = L.inflight.front();
+    const hipError_t q = hipEventQuery(b.done);
+    if (q == hipErrorNotReady) break;
+    for (int32_t s : b.slots) {
+      if (q == hipSuccess) L.index.set_ready(s, b.gen);
+      else L.index.drop(s, b.gen);
+    }
+    (void)hipEventDestroy(b.uploaded);
+    (void)hipEventDestroy(b.done);
+    L.inflight.pop_front();
+  }
+}
+
+// Brackets the next launch on the lane's stream with timing events
+// (sv_timing_enable); lat_timing_end after the launch.
+int lat_timing_begin(LatLane& L, hipEvent_t* e0) {
+  *e0 = nullptr;
+  if (!g_timing.load()) return SV_OK;
+  SV_HIP(hipEventCreate(e0));
+  SV_HIP(hipEventRecord(*e0, L.stream));
+  return SV_OK;
+}
+int lat_timing_end(LatLane& L, hipEvent_t e0, uint64_t n) {
+  if (!e0) return SV_OK;
+  hipEvent_t e1 = nullptr;
+  SV_HIP(hipEventCreate(&e1));
+  SV_HIP(hipEventRecord(e1, L.stream));
+  L.pending.emplace_back(e0, e1);
+  L.pending_n.push_back(n);
+  return SV_OK;
+}
+int lat_harvest(LatLane& L) {
+  for (size_t k = 0; k < L.pending.size(); ++k) {
+    SV_HIP(hipEventSynchronize(L.pending[k].second));
+    float ms = 0;
+    SV_HIP(hipEventElapsedTime(&ms, L.pending[k].first, L.pending[k].second));
+    L.total_ms += ms;
+    L.launches += 1;
+    L.sigs += L.pending_n[k];
+    (void)hipEventDestroy(L.pending[k].first);
+    (void)hipEventDestroy(L.pending[k].second);
+  }
+  L.pending.clear();
+  L.pending_n.clear();
+  return SV_OK;
+}
+
+// Looks up every key of the batch: true iff all are READY (L.kslots holds
+// their slots).  Keys admitted on this sighting are inserted as BUILDING and
+// listed in fresh_pk / fresh_slot for lat_build.
+bool lat_plan(LatLane& L, const HostIn& in, size_t n) {
+  L.fresh_pk.clear();
+  L.fresh_slot.clear();
+  if (!L.cap) return false;
+  const uint64_t now = ++L.tick;
+  L.kslots.resize(n);
+  bool warm = true;
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t* pk = in.pkp(i);
+    int32_t s = L.index.find(pk);
+    if (s >= 0) {
+      L.index.touch(s, now);
+      if (L.index.state(s) == sv::KeyIndex::READY) {
+        L.kslots[i] = (uint32_t)s;
+        continue;
+      }
+      warm = false;  // (its build is still running)
+      continue;
+    }
+    warm = false;
+    if (L.fresh_pk.size() < kMaxBuildsPerBatch && L.index.admit(pk)) {
+      bool ev = false;
+      s = L.index.insert(pk, L.next_gen, now, &ev);
+      if (s >= 0) {
+        L.fresh_pk.push_back(pk);
+        L.fresh_slot.push_back(s);
+        if (ev) ++L.evicted;
+      }
+    }
+  }
+  return warm;
+}
+
+// Queues the table build of the keys lat_plan admitted, after everything
+// already on the lane's stream (a build may overwrite an evicted slot that an
+// earlier comb kernel reads).  A failed build only leaves its keys uncached.
+void lat_build(LatLane& L) {
+  const size_t k = L.fresh_pk.size();
+  if (!k) return;
+  const uint64_t gen = L.next_gen++;
+  LatLane::Build b;
+  b.gen = gen;
+  b.uploaded = b.done = nullptr;
+  b.slots = L.fresh_slot;
+  hipError_t e = hipSuccess;
+  // the previous build's upload has left the pinned buffer before it is rewritten
+  if (!L.inflight.empty()) e = hipEventSynchronize(L.inflight.back().uploaded);
+  uint8_t* h = (uint8_t*)L.h_build.p;
+  if (e == hipSuccess) {
+    for (size_t i = 0; i < k; ++i) {
+      std::memcpy(h + 32 * i, L.fresh_pk[i], 32);
+      const uint32_t s = (uint32_t)L.fresh_slot[i];
+      std::memcpy(h + 32 * k + 4 * i, &s, 4);
+    }
+    e = hipEventCreateWithFlags(&b.uploaded, hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(L.ev_lat, L.stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(L.build, L.ev_lat, 0);
+  if (e == hipSuccess) e = hipMemcpyAsync(L.d_build.p, h, 36 * k, hipMemcpyHostToDevice, L.build);
+  if (e == hipSuccess) e = hipEventRecord(b.uploaded, L.build);
+  if (e == hipSuccess)
+    e = sv_launch_keytab(L.d_build.p, (const uint32_t*)((uint8_t*)L.d_build.p + 32 * k), (uint32_t)k,
+                         (uint32_t*)L.ktab.p, (uint32_t*)L.kstat.p, L.build);
+  if (e == hipSuccess) e = hipEventRecord(b.done, L.build);
+  if (e != hipSuccess) {
+    // (an upload already queued completes on its own; the slots stay uncached)
+    if (b.uploaded) (void)hipEventSynchronize(b.uploaded);
+    for (int32_t s : b.slots) L.index.drop(s, gen);
+    if (b.uploaded) (void)hipEventDestroy(b.uploaded);
+    if (b.done) (void)hipEventDestroy(b.done);
+    return;
+  }
+  L.built += k;
+  L.inflight.push_back(std::move(b));
+}
+
+std::atomic<int> g_lat_trace{-1};
+bool lat_trace() {
+  int v = g_lat_trace.load();
+  if (v < 0) {
+    v = getenv("SV_LAT_TRACE") ? 1 : 0;
+    g_lat_trace.store(v);
+  }
+  return v != 0;
+}
+
+// One latency-bound host batch on the slot's latency lane: pinned image (+
+// the key slots when warm), one H2D, [hash kernel, keys D2H], the comb kernel
+// (every key cached) or the octet kernel, one D2H, one sync.
+int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, KeysReadyFn keys_cb,
+                     void* cb_ctx, bool* cb_done) {
+  LatLane& L = D.lat;
+  int rc;
+  if ((rc = lat_ready(D))) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  lat_cache_ready(L);
+  lat_poll(L);
+  const uint32_t dbg = g_dbg.load() & kKernelDbgMask;
+  // (the lattice test knobs select the octet kernel's code paths)
+  const bool warm = lat_plan(L, in, n) && verdict && dbg == 0;
+  size_t msg_total;
+  const Image im = image_of(in, 0, n, &msg_total);
+  const size_t o_ks = (im.bytes + 3) & ~(size_t)3;
+  const size_t in_bytes = warm ? o_ks + 4 * n : im.bytes;
+  const size_t out_per = (verdict ? 1 : 0) + (keys ? 32 : 0);
+  if ((rc = L.h_in.ensure(in_bytes)) || (rc = L.d_in.ensure(in_bytes)) || (rc = L.h_out.ensure(out_per * n)))
+    return rc;
+  if (verdict && (rc = L.d_out.ensure(n))) return rc;
+  if (keys && (rc = L.d_keys.ensure(32 * n))) return rc;
+  uint8_t* h = (uint8_t*)L.h_in.p;
+  pack(in, 0, n, im, h);
+  if (warm) std::memcpy(h + o_ks, L.kslots.data(), 4 * n);
+  const auto t1 = std::chrono::steady_clock::now();
+  SV_HIP(hipMemcpyAsync(L.d_in.p, h, in_bytes, hipMemcpyHostToDevice, L.stream));
+  uint8_t* d = (uint8_t*)L.d_in.p;
+  const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
+  const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
+  uint8_t* ho = (uint8_t*)L.h_out.p;
+  const bool early = keys_cb && keys && verdict;
+  if (keys) {
+    SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n, L.d_keys.p,
+                          L.stream));
+    if (early) {
+      SV_HIP(hipMemcpyAsync(ho + n, L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, L.stream));
+      SV_HIP(hipEventRecord(L.keys_down, L.stream));
+    }
+  }
+  if (verdict) {
+    const int mode = im.var ? 1 : (in.fixed == 32 ? 0 : 2);
+    hipEvent_t e0;
+    if ((rc = lat_timing_begin(L, &e0))) return rc;
+    if (warm)
+      SV_HIP(sv_launch_comb(mode, sv_comb_spw(n, D.cus), d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
+                            L.d_out.p, (const uint32_t*)(d + o_ks), (const uint32_t*)L.ktab.p,
+                            (const uint32_t*)L.kstat.p, (const uint32_t*)L.ctab, L.stream));
+    else
+      SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
+                              L.d_out.p, nullptr, nullptr, D.btab, dbg, L.stream));
+    if ((rc = lat_timing_end(L, e0, n))) return rc;
+    SV_HIP(hipMemcpyAsync(ho, L.d_out.p, n, hipMemcpyDeviceToHost, L.stream));
+  }
+  if (keys && !early)
+    SV_HIP(hipMemcpyAsync(ho + (verdict ? n : 0), L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, L.stream));
+  SV_HIP(hipEventRecord(L.done, L.stream));
+  if (early) {
+    SV_HIP(hipEventSynchronize(L.keys_down));
+    std::memcpy(keys, ho + n, 32 * n);
+    keys_cb(cb_ctx);
+    *cb_done = true;
+  }
+  lat_build(L);  // (after the verify work: a build waits for it on the device)
+  SV_HIP(hipEventSynchronize(L.done));
+  if (verdict) std::memcpy(verdict, ho, n);
+  if (keys && !early) std::memcpy(keys, ho + (verdict ? n : 0), 32 * n);
+  if (warm) ++L.warm;
+  else ++L.cold;
+  if (lat_trace()) {
+    const auto t2 = std::chrono::steady_clock::now();
+    fprintf(stderr, "SV_LAT_TRACE n=%zu %s plan+pack %.1f us device %.1f us\n", n, warm ? "warm" : "cold",
+            std::chrono::duration<double, std::micro>(t1 - t0).count(),
+            std::chrono::duration<double, std::micro>(t2 - t1).count());
+  }
+  return SV_OK;
+}
+
+int lat_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, KeysReadyFn keys_cb,
+              void* cb_ctx, bool* cb_done) {
+  std::lock_guard<std::mutex> g(D.lat.mu);
+  SV_HIP(hipSetDevice(D.phys));
+  const int rc = lat_slice_locked(D, in, n, verdict, keys, keys_cb, cb_ctx, cb_done);
+  if (rc != SV_OK && D.lat.ready) (void)hipStreamSynchronize(D.lat.stream);  // nothing of this call in flight
+  return rc;
+}
+
 // SHA-256 of a host slice of byte strings on one slot.
 int sha_slice(Device& D, const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n, uint8_t* out) {
   std::lock_guard<std::mutex> g(D.mu);
@@ -752,7 +1134,11 @@ int verify_host(const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, con
   const int path = path_from_flags(opts ? opts->flags : 0u);
   bool cb_done = false;
   if (devs.size() == 1) {
-    rc = host_slice(*devs[0], in, n, verdict, keys, path, keys_cb, cb_ctx, &cb_done);
+    // latency-bound batches (one latency launch) take the slot's latency lane
+    if (resolve_path(path, n) == SV_PATH_LATENCY && n <= stage_chunk())
+      rc = lat_slice(*devs[0], in, n, verdict, keys, keys_cb, cb_ctx, &cb_done);
+    else
+      rc = host_slice(*devs[0], in, n, verdict, keys, path, keys_cb, cb_ctx, &cb_done);
   } else {
     rc = shard(devs, n, [&](Device& D, size_t lo, size_t hi) {
       return host_slice(D, in.sub(lo), hi - lo, verdict ? verdict + lo : nullptr, keys ? keys + 32 * lo : nullptr,
@@ -764,6 +1150,22 @@ int verify_host(const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, con
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Releases every slot (caller holds g_mu).  Lock order: lat.mu, then mu.
+void shutdown_locked() {
+  for (Device* D : g_devs) {
+    std::lock_guard<std::mutex> gl(D->lat.mu);
+    std::lock_guard<std::mutex> gd(D->mu);
+    if (D->lat.ready) {
+      (void)hipSetDevice(D->phys);
+      release_lat(D->lat);
+    }
+    release_device(*D);
+  }
+  for (Device* D : g_devs) delete D;
+  g_devs.clear();
+  g_inited = false;
+}
 
 Device* device_arg(int device) {
   if (device < 0 || device >= (int)g_devs.size()) return nullptr;
@@ -778,19 +1180,15 @@ int sv_init(void) { return ensure_init(); }
 
 void sv_shutdown(void) {
   std::lock_guard<std::mutex> g(g_mu);
-  for (Device* D : g_devs) {
-    std::lock_guard<std::mutex> gd(D->mu);
-    release_device(*D);
-  }
-  for (Device* D : g_devs) delete D;
-  g_devs.clear();
-  g_inited = false;
+  shutdown_locked();
 }
 
 int sv_set_device_map(const int* physical, int count) {
   if (count < 0 || (count > 0 && !physical)) return fail(SV_ERR_INVALID_ARG, "bad device map");
-  sv_shutdown();
+  // teardown and the new map in ONE critical section: a concurrent first use
+  // cannot re-initialise with the old map in between
   std::lock_guard<std::mutex> g(g_mu);
+  shutdown_locked();
   g_map.assign(physical, physical + count);
   int rc = init_locked();
   if (rc != SV_OK) {
@@ -970,10 +1368,28 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
   if (!d_msg) return fail(SV_ERR_INVALID_ARG, "null msg");
   if ((rc = debug_fail())) return rc;
   Device& D = *Dp;
+  hipStream_t user = (hipStream_t)stream;
+  if (resolve_path(SV_PATH_AUTO, n) == SV_PATH_LATENCY) {
+    // the latency lane (octet kernel: the keys are in device memory, so the
+    // host-side key cache is not consulted)
+    LatLane& L = D.lat;
+    std::lock_guard<std::mutex> g(L.mu);
+    SV_HIP(hipSetDevice(D.phys));
+    if ((rc = lat_ready(D))) return rc;
+    SV_HIP(hipEventRecord(L.ev_lat, user));
+    SV_HIP(hipStreamWaitEvent(L.stream, L.ev_lat, 0));
+    hipEvent_t e0;
+    if ((rc = lat_timing_begin(L, &e0))) return rc;
+    SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d_pk, d_sig, d_msg, d_msg_off, d_msg_len, fixed_msg_len, n,
+                            d_verdict, d_bitmap, nullptr, D.btab, g_dbg.load() & kKernelDbgMask, L.stream));
+    if ((rc = lat_timing_end(L, e0, n))) return rc;
+    SV_HIP(hipEventRecord(L.done, L.stream));
+    SV_HIP(hipStreamWaitEvent(user, L.done, 0));
+    return SV_OK;
+  }
   std::lock_guard<std::mutex> g(D.mu);
   SV_HIP(hipSetDevice(D.phys));
   if ((rc = ready_locked(D))) return rc;
-  hipStream_t user = (hipStream_t)stream;
   SV_HIP(hipEventRecord(D.dep_in, user));
   SV_HIP(hipStreamWaitEvent(D.stream, D.dep_in, 0));
   if ((rc = launch_locked(D, mode, SV_PATH_AUTO, d_pk, d_sig, d_msg, d_msg_off, d_msg_len, fixed_msg_len, n,
@@ -1035,18 +1451,21 @@ int sv_kernel_time(int device, double* total_ms, uint64_t* launches, uint64_t* s
   Device* Dp = device_arg(device);
   if (!Dp) return fail(SV_ERR_INVALID_ARG, "device index out of range");
   Device& D = *Dp;
+  std::lock_guard<std::mutex> gl(D.lat.mu);
   std::lock_guard<std::mutex> g(D.mu);
-  if (!D.ready) {
-    if (total_ms) *total_ms = 0;
-    if (launches) *launches = 0;
-    if (signatures) *signatures = 0;
-    return SV_OK;
+  double ms = 0;
+  uint64_t la = 0, sg = 0;
+  if (D.ready) {
+    SV_HIP(hipSetDevice(D.phys));
+    if ((rc = harvest_timing_locked(D))) return rc;
+    if (D.lat.ready && (rc = lat_harvest(D.lat))) return rc;
+    ms = D.total_ms + D.lat.total_ms;
+    la = D.launches + D.lat.launches;
+    sg = D.sigs + D.lat.sigs;
   }
-  SV_HIP(hipSetDevice(D.phys));
-  if ((rc = harvest_timing_locked(D))) return rc;
-  if (total_ms) *total_ms = D.total_ms;
-  if (launches) *launches = D.launches;
-  if (signatures) *signatures = D.sigs;
+  if (total_ms) *total_ms = ms;
+  if (launches) *launches = la;
+  if (signatures) *signatures = sg;
   return SV_OK;
 }
 
@@ -1054,13 +1473,15 @@ int sv_kernel_time_reset(void) {
   int rc = ensure_init();
   if (rc) return rc;
   for (Device* D : g_devs) {
+    std::lock_guard<std::mutex> gl(D->lat.mu);
     std::lock_guard<std::mutex> g(D->mu);
     if (!D->ready) continue;
     (void)hipSetDevice(D->phys);
     if ((rc = harvest_timing_locked(*D))) return rc;
-    D->total_ms = 0;
-    D->launches = 0;
-    D->sigs = 0;
+    if (D->lat.ready && (rc = lat_harvest(D->lat))) return rc;
+    D->total_ms = D->lat.total_ms = 0;
+    D->launches = D->lat.launches = 0;
+    D->sigs = D->lat.sigs = 0;
   }
   return SV_OK;
 }
@@ -1071,10 +1492,59 @@ int sv_device_synchronize(int device) {
   Device* Dp = device_arg(device);
   if (!Dp) return fail(SV_ERR_INVALID_ARG, "device index out of range");
   Device& D = *Dp;
+  std::lock_guard<std::mutex> gl(D.lat.mu);
   std::lock_guard<std::mutex> g(D.mu);
   if (!D.ready) return SV_OK;
   SV_HIP(hipSetDevice(D.phys));
   SV_HIP(hipStreamSynchronize(D.stream));
+  if (D.lat.ready) SV_HIP(hipStreamSynchronize(D.lat.stream));
+  return SV_OK;
+}
+
+int sv_set_key_cache(size_t capacity) {
+  if (capacity > ((size_t)1 << 20)) return fail(SV_ERR_INVALID_ARG, "key cache capacity above 2^20 keys");
+  std::lock_guard<std::mutex> g0(g_mu);
+  g_key_cap.store(capacity);
+  for (Device* D : g_devs) {
+    std::lock_guard<std::mutex> g(D->lat.mu);
+    if (!D->lat.ready) continue;
+    (void)hipSetDevice(D->phys);
+    lat_cache_ready(D->lat);  // (drains the lane, then resizes / clears)
+  }
+  return SV_OK;
+}
+
+int sv_key_cache_wait(int device) {
+  int rc = ensure_init();
+  if (rc) return rc;
+  Device* Dp = device_arg(device);
+  if (!Dp) return fail(SV_ERR_INVALID_ARG, "device index out of range");
+  LatLane& L = Dp->lat;
+  std::lock_guard<std::mutex> g(L.mu);
+  if (!L.ready) return SV_OK;
+  SV_HIP(hipSetDevice(Dp->phys));
+  SV_HIP(hipStreamSynchronize(L.build));
+  lat_poll(L);
+  return SV_OK;
+}
+
+int sv_key_cache_get_stats(int device, sv_key_cache_stats* out) {
+  int rc = ensure_init();
+  if (rc) return rc;
+  Device* Dp = device_arg(device);
+  if (!Dp || !out) return fail(SV_ERR_INVALID_ARG, "bad argument");
+  LatLane& L = Dp->lat;
+  std::lock_guard<std::mutex> g(L.mu);
+  if (L.ready) {
+    (void)hipSetDevice(Dp->phys);
+    lat_poll(L);
+  }
+  out->capacity = L.ready ? L.cap : key_cache_cap();
+  out->keys = L.index.size();
+  out->warm_batches = L.warm;
+  out->cold_batches = L.cold;
+  out->keys_built = L.built;
+  out->evictions = L.evicted;
   return SV_OK;
 }
 

@@ -19,6 +19,7 @@
 
 #include "verify_core.h"
 #include "quad.h"
+#include "sv_kparams.h"
 
 #define SV_BLOCK 256
 #ifndef SV_STAGE_A
@@ -39,20 +40,6 @@
 #endif
 // base-point tables in the device buffer: e·B, then (SV_LATTICE) e·(2^128 B)
 
-struct sv_kparams {
-  const sv_u4* pk;        // n x 32 B (2 quads)
-  const sv_u4* sig;       // n x 64 B (4 quads)
-  const uint8_t* msg;     // fixed: n x fixed_len ; var: msg bytes
-  const uint64_t* msg_off;
-  const uint32_t* msg_len;
-  uint64_t n;
-  uint32_t fixed_len;     // 0 = variable-length
-  uint8_t* verdict;       // n bytes
-  uint64_t* bitmap;       // optional, ceil(n/64) words
-  sv_u4* ws;              // workspace: grid threads x SV_SLOT_QUADS (lane-major)
-  const sv_u4* btab;      // SV_BTAB_ENTRIES x 9 quads (global copy)
-  uint32_t dbg;           // SV_DBG_* test knobs (sv_set_debug_flags), 0 in production
-};
 // test knobs (include/stellar_sigverify.h sv_set_debug_flags)
 #define SV_DBG_TRIVIAL_PAIR 1u  // every lane takes the fallback pair (h, 1)
 #define SV_DBG_MAX_WINDOWS 2u   // every wave runs 64 windows
@@ -66,31 +53,6 @@ __device__ __forceinline__ int sv_wave_windows(int wl, uint32_t dbg) {
 __device__ __forceinline__ void sv_load_btab_lds(sv_u4* s_btab, const sv_u4* g_btab) {
   for (int i = threadIdx.x; i < SV_BTAB_ENTRIES * (SV_BTAB_STRIDE / 4); i += blockDim.x) s_btab[i] = g_btab[i];
   __syncthreads();
-}
-
-__device__ __forceinline__ void sv_unpack2(uint32_t w[8], const sv_u4* p) {
-  const sv_u4 a = p[0], b = p[1];
-  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
-  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-}
-
-// Loads one signature's inputs and hashes R || A || M (step (6)).
-template <int MODE>
-__device__ __forceinline__ void sv_load_and_hash(const sv_kparams& p, uint64_t ii, uint32_t A[8], uint32_t S[8],
-                                                 uint32_t hram[16]) {
-  uint32_t R[8];
-  sv_unpack2(A, p.pk + 2 * ii);
-  sv_unpack2(R, p.sig + 4 * ii);
-  sv_unpack2(S, p.sig + 4 * ii + 2);
-  if (MODE == 0) {
-    uint32_t M[8];
-    sv_unpack2(M, (const sv_u4*)(p.msg) + 2 * ii);
-    sha512_ram32(hram, R, A, M);
-  } else if (MODE == 1) {
-    sha512_ram_var(hram, R, A, p.msg + p.msg_off[ii], p.msg_len[ii]);
-  } else {
-    sha512_ram_var(hram, R, A, p.msg + ii * (uint64_t)p.fixed_len, p.fixed_len);
-  }
 }
 
 // Each wave iteration handles SV_BATCH_K groups of 64 consecutive signatures

@@ -1,0 +1,46 @@
+// Verify-launch parameters and the per-signature input loader shared by the
+// kernel translation units (sv_kernels.hip, sv_comb.hip).
+#pragma once
+
+#include "verify_core.h"
+
+struct sv_kparams {
+  const sv_u4* pk;        // n x 32 B (2 quads)
+  const sv_u4* sig;       // n x 64 B (4 quads)
+  const uint8_t* msg;     // fixed: n x fixed_len ; var: msg bytes
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  uint64_t n;
+  uint32_t fixed_len;     // 0 = variable-length
+  uint8_t* verdict;       // n bytes
+  uint64_t* bitmap;       // optional, ceil(n/64) words
+  sv_u4* ws;              // workspace: grid threads x SV_SLOT_QUADS (lane-major)
+  const sv_u4* btab;      // SV_BTAB_ENTRIES x 9 quads (global copy)
+  uint32_t dbg;           // SV_DBG_* test knobs (sv_set_debug_flags), 0 in production
+};
+
+__device__ __forceinline__ void sv_unpack2(uint32_t w[8], const sv_u4* p) {
+  const sv_u4 a = p[0], b = p[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+// Loads one signature's inputs and hashes R || A || M (step (6)).
+// MODE 0: fixed 32-byte messages, 1: variable length, 2: fixed other length.
+template <int MODE>
+__device__ __forceinline__ void sv_load_and_hash(const sv_kparams& p, uint64_t ii, uint32_t A[8], uint32_t S[8],
+                                                 uint32_t hram[16]) {
+  uint32_t R[8];
+  sv_unpack2(A, p.pk + 2 * ii);
+  sv_unpack2(R, p.sig + 4 * ii);
+  sv_unpack2(S, p.sig + 4 * ii + 2);
+  if (MODE == 0) {
+    uint32_t M[8];
+    sv_unpack2(M, (const sv_u4*)(p.msg) + 2 * ii);
+    sha512_ram32(hram, R, A, M);
+  } else if (MODE == 1) {
+    sha512_ram_var(hram, R, A, p.msg + p.msg_off[ii], p.msg_len[ii]);
+  } else {
+    sha512_ram_var(hram, R, A, p.msg + ii * (uint64_t)p.fixed_len, p.fixed_len);
+  }
+}

@@ -251,3 +251,220 @@ extern "C" int hc_stub_keyed(const uint8_t*, const uint8_t* sig, const uint8_t*,
   for (size_t i = 0; i < n; ++i) memcpy(keys + 32 * i, sig + 64 * i, 32);
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Warm-key latency path (stellar-core_amd/csrc/comb.h): a host model of the
+// comb kernel's algorithm over the same table layout -- per-key tables of
+// d * 16^j * (-A), base tables of e * 256^j * B, signed digits of h and S,
+// the sum of 96 entries (the first one taken as the point 2X:2Y:2Z:2T, as the
+// kernel does), and the projective test against the decoded R.  Pins the
+// equation and the layout on CPU before the GPU runs the own-form version.
+#include "../../stellar-core_amd/csrc/comb_core.h"
+#include "../../stellar-core_amd/csrc/keycache.h"
+
+#include <map>
+#include <random>
+#include <string>
+
+static std::vector<uint32_t> g_cb;
+static std::once_flag g_cb_once;
+
+
+static void init_cb() {
+  g_cb.assign(SV_CB_DW, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < 8; ++t)
+    th.emplace_back([t] {
+      for (int id = t; id < SV_CB_POS * SV_CB_ENT; id += 8)
+        sv_comb_bentry(&g_cb[(size_t)id * SV_CE_DW], id / SV_CB_ENT, id % SV_CB_ENT);
+    });
+  for (auto& x : th) x.join();
+}
+
+// tables of -A (layout of one key-cache slot); returns the key status
+static uint32_t keytab_host(uint32_t* tab, const uint32_t A[8]) {
+  bool ok = sv_point_canonical(A) && !sv_small_order(A);
+  ge_p3 P;
+  ok = ge_frombytes(P, A, true) && ok;
+  ge_p1p1 Q;
+  ge_cached id;
+  ge_cached_identity(id);
+  for (int j = 0; j < SV_KA_POS; ++j) {
+    uint32_t* pe = tab + (size_t)j * SV_KA_ENT * SV_CE_DW;
+    ge_cached c1, ce;
+    ge_p3_to_cached(c1, P);
+    sv_ce_put(pe, id);
+    sv_ce_put(pe + SV_CE_DW, c1);
+    ge_p3 acc = P;
+    for (int e = 2; e < SV_KA_ENT; ++e) {
+      ge_add_preswapped(Q, acc, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, false);
+      ge_p1p1_to_p3(acc, Q);
+      ge_p3_to_cached(ce, acc);
+      sv_ce_put(pe + e * SV_CE_DW, ce);
+    }
+    for (int k = 0; k < 4; ++k) {
+      ge_dbl(Q, P.X, P.Y, P.Z);
+      ge_p1p1_to_p3(P, Q);
+    }
+  }
+  return ok ? SV_KEY_OK : SV_KEY_BAD;
+}
+
+static bool comb_verify_one(const uint32_t* ktab, uint32_t kst, const uint8_t* pk, const uint8_t* sig,
+                            const uint8_t* msg, uint32_t mlen) {
+  uint32_t A[8], R[8], S[8], hram[16], h[8], dA[8], dB[8];
+  load_words(A, pk);
+  load_words(R, sig);
+  load_words(S, sig + 32);
+  sha512_ram_var(hram, R, A, msg, mlen);
+  sc_reduce512(h, hram);
+  const bool s_ok = sc_is_canonical(S);
+  S[7] &= 0x0fffffffu;
+  sc_digits_r16(dA, h);
+  sc_digits_r256(dB, S);
+  ge_p3 P;
+  ge_p1p1 Q;
+  bool first = true;
+  auto add = [&](const uint32_t* ent, bool neg) {
+    ge_cached c;
+    sv_ce_get(c, ent, neg);
+    if (first) {
+      // 2 * the entry's point: ((Y+X)-(Y-X), (Y+X)+(Y-X), 2Z, 2dT / d)
+      fe dinv;
+      fe_const_dinv(dinv);
+      fe_sub(P.X, c.YpX, c.YmX);
+      fe_add(P.Y, c.YpX, c.YmX);
+      fe_add(P.Z, c.Z, c.Z);
+      fe_mul(P.T, c.T2d, dinv);
+      if (neg) {
+        fe nt;
+        fe_neg(nt, P.T);
+        P.T = nt;
+      }
+      fe_weak(P.X); fe_weak(P.Y); fe_weak(P.Z); fe_weak(P.T);
+      first = false;
+      return;
+    }
+    ge_add_preswapped(Q, P, c.YpX, c.YmX, c.Z, c.T2d, neg, false);
+    ge_p1p1_to_p3(P, Q);
+  };
+  for (int j = 0; j < SV_KA_POS; ++j) {
+    const int32_t d = (int32_t)(dA[j >> 3] << (28 - 4 * (j & 7))) >> 28;
+    add(ktab + ((size_t)j * SV_KA_ENT + (uint32_t)(d < 0 ? -d : d)) * SV_CE_DW, d < 0);
+  }
+  for (int j = 0; j < SV_CB_POS; ++j) {
+    const int32_t e = (int32_t)(dB[j >> 2] << (24 - 8 * (j & 3))) >> 24;
+    add(&g_cb[((size_t)j * SV_CB_ENT + (uint32_t)(e < 0 ? -e : e)) * SV_CE_DW], e < 0);
+  }
+  bool r_ok = !sv_small_order(R) && sv_point_canonical(R);
+  ge_p3 Rp;
+  r_ok = ge_frombytes(Rp, R, false) && r_ok;
+  fe t, dx, dy;
+  fe_mul(t, Rp.X, P.Z);
+  fe_sub(dx, P.X, t);
+  fe_mul(t, Rp.Y, P.Z);
+  fe_sub(dy, P.Y, t);
+  return fe_iszero(dx) && fe_iszero(dy) && r_ok && s_ok && kst == SV_KEY_OK;
+}
+
+extern "C" void hc_comb_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                                     const uint32_t* len, size_t n, uint8_t* out) {
+  std::call_once(g_cb_once, init_cb);
+  // one table per distinct key, built in parallel
+  std::map<std::string, size_t> slot;
+  std::vector<size_t> key_of(n);
+  for (size_t i = 0; i < n; ++i) {
+    auto it = slot.emplace(std::string((const char*)pk + 32 * i, 32), slot.size()).first;
+    key_of[i] = it->second;
+  }
+  const size_t nk = slot.size();
+  std::vector<uint32_t> tabs(nk * (size_t)SV_KEY_SLOT_DW), stat(nk);
+  std::vector<const uint8_t*> kp(nk);
+  for (size_t i = 0; i < n; ++i) kp[key_of[i]] = pk + 32 * i;
+  std::vector<std::thread> th;
+  for (int t = 0; t < 8; ++t)
+    th.emplace_back([&, t] {
+      for (size_t k = t; k < nk; k += 8) {
+        uint32_t A[8];
+        load_words(A, kp[k]);
+        stat[k] = keytab_host(&tabs[k * SV_KEY_SLOT_DW], A);
+      }
+    });
+  for (auto& x : th) x.join();
+  th.clear();
+  for (int t = 0; t < 8; ++t)
+    th.emplace_back([&, t] {
+      for (size_t i = t; i < n; i += 8)
+        out[i] = comb_verify_one(&tabs[key_of[i] * SV_KEY_SLOT_DW], stat[key_of[i]], pk + 32 * i, sig + 64 * i,
+                                 msg + off[i], len[i])
+                     ? 1
+                     : 0;
+    });
+  for (auto& x : th) x.join();
+}
+
+// KeyIndex (csrc/keycache.h) against a map model under random traffic:
+// returns 0, or a nonzero code naming the first inconsistency.
+extern "C" int hc_keyindex_fuzz(uint64_t seed, int cap, int ops, int universe) {
+  sv::KeyIndex ix;
+  ix.reset((size_t)cap);
+  std::mt19937_64 rng(seed);
+  std::map<std::string, int32_t> model;  // key -> slot (present in the index)
+  auto key = [](int k) {
+    std::string s(32, '\0');
+    uint64_t x = 0x9e3779b97f4a7c15ull * (uint64_t)(k + 1);
+    for (int i = 0; i < 32; ++i) {
+      x ^= x >> 31;
+      x *= 0xbf58476d1ce4e5b9ull;
+      s[i] = (char)(x >> 56);
+    }
+    // adversarial flavour: a quarter of the keys share their first 16 bytes
+    if (k % 4 == 0) std::memset(&s[0], 0x5a, 16);
+    return s;
+  };
+  uint64_t now = 0, gen = 0;
+  for (int op = 0; op < ops; ++op) {
+    ++now;
+    const int k = (int)(rng() % (uint64_t)universe);
+    const std::string kb = key(k);
+    const uint8_t* p = (const uint8_t*)kb.data();
+    const int32_t s = ix.find(p);
+    auto it = model.find(kb);
+    if ((s >= 0) != (it != model.end())) return 1;
+    if (s >= 0) {
+      if (it->second != s) return 2;
+      if (std::memcmp(ix.key(s), p, 32) != 0) return 3;
+      ix.touch(s, now);
+      if (ix.state(s) == sv::KeyIndex::BUILDING && rng() % 2) ix.set_ready(s, ix.gen(s));
+      continue;
+    }
+    if (!ix.admit(p)) continue;
+    bool ev = false;
+    const int32_t t = ix.insert(p, ++gen, now, &ev);
+    if (t < 0) continue;
+    if (ev) {
+      // the victim must have left the model (exactly one key maps to t)
+      int gone = 0;
+      for (auto m = model.begin(); m != model.end();)
+        if (m->second == t) {
+          m = model.erase(m);
+          ++gone;
+        } else {
+          ++m;
+        }
+      if (gone != 1) return 4;
+    }
+    model[kb] = t;
+    if ((int)ix.size() != (int)model.size()) return 5;
+    if ((int)ix.size() > cap) return 6;
+    if (rng() % 8 == 0) ix.drop(t, gen), model.erase(kb);
+  }
+  // every model key still found, slots distinct
+  std::vector<int> used((size_t)cap, 0);
+  for (auto& m : model) {
+    if (ix.find((const uint8_t*)m.first.data()) != m.second) return 7;
+    if (used[(size_t)m.second]++) return 8;
+  }
+  return (int)ix.size() == (int)model.size() ? 0 : 9;
+}
+

@@ -1,0 +1,166 @@
+"""GPU parity of the warm-key latency path (csrc/sv_comb.hip, csrc/comb.h).
+
+A latency-path host batch whose public keys are all in the device's key cache
+runs the comb kernel; every other batch runs the octet kernel and queues its
+keys for a table build.  Both must give libsodium's verdict on every row:
+  * every golden fixture class (reference in-tree vectors, libsodium-signed
+    valid rows, message lengths 0..512, every adversarial class including
+    small-order / non-canonical / off-curve keys, which the cache records as
+    rejecting keys), first cold, then warm;
+  * an SCP-shaped set (100 validator keys, 0..400-byte messages, mutated rows)
+    at sizes that select each kernel geometry (1, 2 and 4 signatures per
+    chain wave), against the oracle;
+  * eviction: a cache smaller than the key set still gives exact verdicts.
+"""
+import numpy as np
+import pytest
+
+from conftest import oracle_verdicts
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu(sv):
+    if sv.device_count() < 1:
+        pytest.skip("no GPU")
+    return 0
+
+
+@pytest.fixture
+def cache(sv, gpu):
+    sv.set_key_cache(8192)
+    yield sv
+    sv.set_key_cache(1024)
+
+
+def _run(sv, d, rows=None):
+    pk, sig, off, ln = d["pk"], d["sig"], d["msg_off"], d["msg_len"]
+    if rows is not None:
+        pk, sig, off, ln = pk[rows], sig[rows], off[rows], ln[rows]
+    return sv.verify_batch(pk, sig, d["msg"], off, ln, device=0, path="latency")
+
+
+def _warm_up(sv, d, want, rounds=16):
+    """Runs the batch until it is served warm; every run must be exact."""
+    for r in range(rounds):
+        w0 = sv.key_cache_stats(0)["warm_batches"]
+        out = _run(sv, d)
+        assert (out == want).all(), "round %d: %s" % (r, np.nonzero(out != want)[0][:10])
+        if sv.key_cache_stats(0)["warm_batches"] == w0 + 1:
+            return r
+        sv.key_cache_wait(0)
+    raise AssertionError("batch never ran warm: %s" % sv.key_cache_stats(0))
+
+
+@pytest.mark.parametrize("name", ["intree", "valid", "msglen", "adversarial", "lattice_edge"])
+def test_golden_fixtures_warm(sv, cache, golden, name):
+    d = golden[name]
+    r = _warm_up(sv, d, d["verdict"])
+    assert r >= 1  # (the first run is cold: its keys were unknown)
+    out = _run(sv, d)  # warm again
+    bad = np.nonzero(out != d["verdict"])[0]
+    assert len(bad) == 0, [(int(i), str(d["class_names"][d["cls"][i]])) for i in bad[:10]]
+
+
+def _scp_set(oracle, n, seed):
+    import ctypes
+    rng = np.random.default_rng(seed)
+    keys = []
+    for v in range(100):
+        seedb = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        pkb, skb = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+        oracle.oracle_ed25519_seed_keypair(pkb, skb, seedb)
+        keys.append((pkb.raw, skb.raw))
+    pk = np.zeros((n, 32), np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    msgs, lens = [], []
+    for i in range(n):
+        pkb, skb = keys[int(rng.integers(0, 100))]
+        m = rng.integers(0, 256, int(rng.integers(0, 401)), dtype=np.uint8).tobytes()
+        sb = ctypes.create_string_buffer(64)
+        oracle.oracle_ed25519_sign(sb, m, len(m), skb)
+        s = bytearray(sb.raw)
+        kind = int(rng.integers(0, 10))
+        if kind == 0:
+            s[int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))  # R bit
+        elif kind == 1:
+            s[32 + int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))  # S bit
+        elif kind == 2 and m:
+            m = bytes([m[0] ^ 1]) + m[1:]
+        pk[i] = np.frombuffer(pkb, np.uint8)
+        sig[i] = np.frombuffer(bytes(s), np.uint8)
+        msgs.append(m)
+        lens.append(len(m))
+    ln = np.array(lens, np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(msgs), np.uint8) if sum(lens) else np.zeros(1, np.uint8)
+    d = {"pk": pk, "sig": sig, "msg": buf, "msg_off": off, "msg_len": ln}
+    d["verdict"] = oracle_verdicts(oracle, d, rows=range(n))
+    return d
+
+
+@pytest.mark.parametrize("n", [1, 7, 500, 1200, 3000])
+def test_scp_set_geometries(sv, cache, oracle, n):
+    """n = 1..768 runs 1 signature per chain wave, up to 1536 two, above four
+    (sv_comb_spw); tails of the last workgroup are exercised by odd n."""
+    d = _scp_set(oracle, n, seed=n)
+    assert 0 < int(d["verdict"].sum()) <= n
+    _warm_up(sv, d, d["verdict"])
+    out = _run(sv, d)
+    assert (out == d["verdict"]).all()
+
+
+def test_fixed32_messages_warm(sv, cache, golden):
+    """The fixed-length entry point (32-byte tx hashes, MODE 0) on the comb kernel."""
+    d = golden["valid"]
+    rows = np.nonzero(d["msg_len"] == 32)[0]
+    assert len(rows) > 100
+    msg = np.stack([d["msg"][int(d["msg_off"][i]):int(d["msg_off"][i]) + 32] for i in rows])
+    pk, sig = d["pk"][rows], d["sig"][rows]
+    for _ in range(8):
+        w0 = sv.key_cache_stats(0)["warm_batches"]
+        out = sv.verify_fixed(pk, sig, msg, 32, device=0, path="latency")
+        assert out.all()
+        if sv.key_cache_stats(0)["warm_batches"] == w0 + 1:
+            break
+        sv.key_cache_wait(0)
+    else:
+        raise AssertionError("never warm")
+    sig2 = sig.copy()
+    sig2[::3, 40] ^= 4
+    out = sv.verify_fixed(pk, sig2, msg, 32, device=0, path="latency")
+    want = np.ones(len(rows), np.uint8)
+    want[::3] = 0
+    assert (out == want).all()
+
+
+def test_small_cache_evicts_exactly(sv, gpu, oracle):
+    """A 64-key cache under a 100-key workload keeps evicting; verdicts stay
+    exact whichever kernel serves each batch."""
+    sv.set_key_cache(64)
+    try:
+        for seed in range(6):
+            d = _scp_set(oracle, 300, seed=1000 + seed)
+            for _ in range(2):
+                out = _run(sv, d)
+                assert (out == d["verdict"]).all()
+                sv.key_cache_wait(0)
+        st = sv.key_cache_stats(0)
+        assert st["capacity"] == 64 and st["keys"] <= 64
+        assert st["evictions"] > 0
+    finally:
+        sv.set_key_cache(1024)
+
+
+def test_cache_off_is_octet_only(sv, gpu, golden):
+    sv.set_key_cache(0)
+    try:
+        d = golden["adversarial"]
+        w0 = sv.key_cache_stats(0)["warm_batches"]
+        for _ in range(3):
+            assert (_run(sv, d) == d["verdict"]).all()
+        assert sv.key_cache_stats(0)["warm_batches"] == w0
+    finally:
+        sv.set_key_cache(1024)
