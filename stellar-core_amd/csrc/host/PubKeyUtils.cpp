@@ -217,14 +217,19 @@ class RandomEvictionCache {
   }
   // fills in a pending value if entry `id` still holds this batch's item (it
   // may have been evicted and its id reused since)
+  // (clearVerifySigCache between a batch's walk and its resolve leaves ids
+  // past the cleared table: nothing to fill in then)
   void resolve(uint32_t id, uint64_t owner, uint32_t pendIdx, bool v) {
+    if (id >= entries_.size()) return;
     Entry& e = entries_[id];
     if (e.owner == owner && e.pendIdx == pendIdx) {
       e.value = v;
       e.owner = 0;
     }
   }
-  void prefetchEntry(uint32_t id) const { __builtin_prefetch(&entries_[id], 1); }
+  void prefetchEntry(uint32_t id) const {
+    if (id < entries_.size()) __builtin_prefetch(&entries_[id], 1);
+  }
   void clear() {
     std::fill(table_.begin(), table_.end(), 0u);
     entries_.clear();

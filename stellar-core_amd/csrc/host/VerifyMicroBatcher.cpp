@@ -2,6 +2,7 @@
 #include "VerifyMicroBatcher.h"
 
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <exception>
 
@@ -50,21 +51,31 @@ void VerifyMicroBatcher::enqueue(PublicKey const& key, ByteSlice const& sig, Byt
   r.msgLen = (uint32_t)msg.size();
   r.done = done;
   if (mRecordLatency) r.t0 = Clock::now();
+  r.arrivalNs = nowNs();
+  size_t q;
   {
     Shard& sh = mShards[tShard];
     std::lock_guard<std::mutex> g(sh.mu);
     r.msgOff = sh.q.arena.size();
     sh.q.arena.insert(sh.q.arena.end(), msg.begin(), msg.end());
     sh.q.recs.push_back(r);
+    // counted under the shard lock: a worker that takes this record (under
+    // the same lock) always finds it counted, so its fetch_sub never wraps
+    mEnqueued.fetch_add(1);
+    q = mQueued.fetch_add(1) + 1;
+    if (q == 1) mOldestNs.store(r.arrivalNs);
   }
-  mEnqueued.fetch_add(1);
-  const size_t q = mQueued.fetch_add(1) + 1;
-  if (q == 1) {
-    mOldestNs.store(nowNs());
-    wake();
-  } else if (q == mMaxBatch) {
-    wake();
+  if (q == 1 || q == mMaxBatch) wake();
+}
+
+int64_t VerifyMicroBatcher::oldestQueuedNs() {
+  int64_t oldest = INT64_MAX;
+  for (size_t s = 0; s < kShards; ++s) {
+    Shard& sh = mShards[s];
+    std::lock_guard<std::mutex> g(sh.mu);
+    if (!sh.q.recs.empty()) oldest = std::min(oldest, sh.q.recs.front().arrivalNs);  // (FIFO per shard)
   }
+  return oldest;
 }
 
 std::future<bool> VerifyMicroBatcher::submit(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg) {
@@ -149,7 +160,9 @@ void VerifyMicroBatcher::run() {
     start = (start + 1) % kShards;
     const size_t left = mQueued.fetch_sub(take) - take;
     if (left > 0) {
-      mOldestNs.store(nowNs());  // (an upper bound for the leftovers' arrival)
+      // the leftovers keep their own deadline: the oldest one's arrival
+      const int64_t oldest = oldestQueuedNs();
+      if (oldest != INT64_MAX) mOldestNs.store(oldest);
       if (left >= mMaxBatch) wake();
     }
     if (take == 0) {

@@ -79,7 +79,9 @@ class VerifyMicroBatcher {
     uint64_t msgOff;           // into the arena
     std::promise<bool>* done;  // submit() only
     Clock::time_point t0;      // recordLatency only
+    int64_t arrivalNs;         // deadline accounting (steady clock)
   };
+  int64_t oldestQueuedNs();  // arrival of the oldest queued record (INT64_MAX: none)
   struct Queue {
     std::vector<Rec> recs;
     std::vector<uint8_t> arena;

@@ -113,5 +113,6 @@ def case_set(case):
     es = EnvelopeSet()
     for a in case["accounts"]:
         es.account(a)
-    es.envelope(case["source"], case["hash"], case["sigs"], case["ops"], fee_bump=case.get("fee_bump"))
+    es.envelope(case["source"], case["hash"], case["sigs"], case["ops"], extra=case.get("extra", ()),
+                fee_bump=case.get("fee_bump"))
     return es

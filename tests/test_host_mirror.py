@@ -164,6 +164,46 @@ def test_verify_sig_batch_dedup_and_verdicts(host, engine, golden):
     assert _counts(host) == (20, n - 20)
 
 
+def test_cache_cleared_during_batch(host, oracle, golden):
+    """clearVerifySigCache between a batch's cache walk and the resolve of its
+    pending inserts (here: from inside the engine call) must neither touch the
+    cleared table nor change the batch's verdicts (resolve() bounds)."""
+    e = OracleEngine(oracle)
+
+    def clearing(*a):
+        host.svh_cache_clear()
+        return e.fn_plain(*a)
+
+    cfn = VERIFY_FN(clearing)
+    d = golden["adversarial"]
+    rows = np.concatenate([np.arange(0, 600, 3), np.arange(0, 60, 3)])  # with in-batch duplicates
+    n = len(rows)
+    pk, sig = np.ascontiguousarray(d["pk"][rows]), np.ascontiguousarray(d["sig"][rows])
+    off, ln = np.ascontiguousarray(d["msg_off"][rows]), np.ascontiguousarray(d["msg_len"][rows])
+    msg = np.ascontiguousarray(d["msg"])
+    vp = ctypes.c_void_p
+    host.svh_set_test_verifier(ctypes.cast(cfn, ctypes.c_void_p))
+    try:
+        for _ in range(3):
+            host.svh_cache_clear()
+            out = np.zeros(n, np.uint8)
+            assert host.svh_verify_sig_batch(vp(pk.ctypes.data), vp(sig.ctypes.data), None, vp(msg.ctypes.data),
+                                             vp(off.ctypes.data), vp(ln.ctypes.data), ctypes.c_size_t(n),
+                                             vp(out.ctypes.data)) == 0
+            assert (out == d["verdict"][rows]).all()
+            assert host.svh_cache_keys(None, 0) == 0  # cleared mid-batch: nothing of it was resolved in
+        # the cache keeps working afterwards
+        host.svh_set_test_verifier(ctypes.cast(e.cfn, ctypes.c_void_p))
+        out = np.zeros(n, np.uint8)
+        assert host.svh_verify_sig_batch(vp(pk.ctypes.data), vp(sig.ctypes.data), None, vp(msg.ctypes.data),
+                                         vp(off.ctypes.data), vp(ln.ctypes.data), ctypes.c_size_t(n),
+                                         vp(out.ctypes.data)) == 0
+        assert (out == d["verdict"][rows]).all()
+    finally:
+        host.svh_set_test_verifier(None)
+        host.svh_cache_clear()
+
+
 def test_verify_sig_batch_keyed_path(host, oracle, golden):
     """f4: with the keyed pass (verdicts + cache keys from the engine, no host
     hashing) verdicts, hit/miss counters and cache contents match the hashed

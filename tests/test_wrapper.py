@@ -5,7 +5,10 @@ tests/golden/make_wrapper.py with libsodium 1.0.18):
   SignatureUtilsTest.cpp:15-32   100 NODE_SEED_i / HASH_ij round trips
   SignatureUtilsTest.cpp:34-48   HASH_X signers for x = 'A' * 0..64
   CryptoTests.cpp:272-297        "sign tests"
-  TxEnvelopeTests.cpp:396-736    outer-envelope and multisig outcomes
+  TxEnvelopeTests.cpp:98-1637    payload signers, extraSigners, outer-envelope,
+                                 multisig and "alternative signatures" outcomes
+  FeeBumpTransactionTests.cpp:117-216  fee-bump outer / inner outcomes
+  HerderTests.cpp:2052-2115      StellarValue signatures
 
 CPU tests run the C++ mirror with verification on the engine's CPU path (no
 GPU, no test double); the `gpu` variants force every verification through
@@ -118,10 +121,15 @@ def _all_wrapper_checks(host, prefetch):
     assert _sign_test_calls(host) == [r["expect"] for r in WRAPPER["sign_tests"]], "CryptoTests.cpp:272-297"
     for case in WRAPPER["envelopes"]:
         for proto, want in case["expect"].items():
-            _check_expect(_envelope_results(host, case, int(proto), prefetch), want, (case["name"], proto, prefetch))
+            if not case.get("apply_only"):
+                _check_expect(_envelope_results(host, case, int(proto), prefetch), want,
+                              (case["name"], proto, prefetch))
             if proto == "21":  # the apply path (processSignatures) reaches the same outcome
                 _check_expect(_envelope_results(host, case, 21, prefetch, for_apply=1), want,
                               (case["name"], "apply", prefetch))
+    for r in WRAPPER["value_sigs"]:  # HerderTests.cpp:2052-2115 through verifySig
+        m, sg = bytes.fromhex(r["msg"]), bytes.fromhex(r["sig"])
+        assert host.svh_verify_sig(bytes.fromhex(r["pk"]), sg or bytes(1), len(sg), m, len(m)) == r["expect"], r
 
 
 def test_wrapper_fixtures_cpu_path(host):
@@ -137,6 +145,25 @@ def test_wrapper_fixtures_cpu_path(host):
         host.svh_set_cpu_threshold(1)
     s = engine_stats(host)
     assert s.gpu_signatures == 0 and s.cpu_signatures > 0
+
+
+def test_python_replay_matches_reference_outcomes(oracle):
+    """tests/txset_gen.py replay_envelope (an independent restatement of the
+    reference's transaction-level checks) reaches every outcome wrapper.json
+    pins, in both modes -- the same fixtures the C++ mirror is held to."""
+    def verify(pk, sig, msg):
+        return oracle.oracle_ed25519_verify(sig, msg, len(msg), pk) == 0
+
+    n = 0
+    for case in WRAPPER["envelopes"]:
+        for proto, want in case["expect"].items():
+            modes = ([] if case.get("apply_only") else [0]) + ([1] if proto == "21" else [])
+            for mode in modes:
+                got = tg.replay_envelope(case, int(proto), mode, verify)
+                for k, v in want.items():
+                    assert got[k] == v, (case["name"], proto, mode, k, got, want)
+                n += 1
+    assert n > 150
 
 
 def test_envelope_hint_and_size_rules_need_no_verification(host):

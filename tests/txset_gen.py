@@ -195,3 +195,144 @@ def replay(txs, verify):
         ok.append(1 if done else 0)
         used_all.append(1 if all(used) else 0)
     return np.array(ok, np.uint8), np.array(used_all, np.uint8)
+
+
+# ---------------------------------------------------------------------------
+# Transaction-level replay (tests/golden/wrapper.json "envelopes"): an
+# independent Python restatement of the reference's signature checks of one
+# envelope -- TransactionFrame.cpp:268-321 (checkSignature /
+# checkSignatureNoAccount / checkExtraSigners), :1091-1156 (processSignatures),
+# :1247-1262 (commonValid), OperationFrame.cpp:173-209 and
+# FeeBumpTransactionFrame.cpp:138-197 -- over ONE checker per envelope whose
+# used-signature marks persist across its calls (SignatureChecker.cpp:30-158).
+
+TX_NO_ACCOUNT, TX_BAD_AUTH, TX_BAD_AUTH_EXTRA, TX_FAILED = -8, -6, -10, -1
+OP_BAD_AUTH, OP_NO_ACCOUNT = -1, -2
+
+
+class Checker:
+    def __init__(self, protocol, contents_hash, sigs, verify):
+        self.protocol, self.hash, self.sigs, self.verify = protocol, contents_hash, sigs, verify
+        self.used = [False] * len(sigs)
+
+    def check(self, signers, needed):
+        if self.protocol == 7:
+            return True
+        by = {ED25519: [], PRE_AUTH_TX: [], HASH_X: [], SIGNED_PAYLOAD: []}
+        for g in signers:
+            by[g["type"]].append(g)
+        clamp = (lambda w: min(w, 255)) if self.protocol >= 10 else (lambda w: w)
+        total = 0
+        for g in by[PRE_AUTH_TX]:
+            if g["key"] == self.hash:
+                total += clamp(g["weight"])
+                if total >= needed:
+                    return True
+
+        def run(signers_, match):
+            nonlocal total
+            for i, s in enumerate(self.sigs):
+                for g in list(signers_):
+                    if match(s, g):
+                        self.used[i] = True
+                        total += clamp(g["weight"])
+                        if total >= needed:
+                            return True
+                        signers_.remove(g)
+                        break
+            return False
+
+        def hx(s, g):
+            return s["hint"] == hint_of(g["key"]) and hashlib.sha256(s["sig"]).digest() == g["key"]
+
+        def ed(s, g):
+            return s["hint"] == hint_of(g["key"]) and len(s["sig"]) == 64 and self.verify(g["key"], s["sig"], self.hash)
+
+        def sp(s, g):
+            return (self.protocol >= 19 and s["hint"] == payload_hint(g["key"], g["payload"]) and len(s["sig"]) == 64
+                    and self.verify(g["key"], s["sig"], g["payload"]))
+
+        return run(by[HASH_X], hx) or run(by[ED25519], ed) or run(by[SIGNED_PAYLOAD], sp)
+
+    def all_used(self):
+        return self.protocol == 7 or all(self.used)
+
+
+def _signers_of(acc):
+    out = []
+    if acc["thresholds"][0]:
+        out.append({"type": ED25519, "key": acc["id"], "weight": acc["thresholds"][0], "payload": b""})
+    return out + [dict(g) for g in acc["signers"]]
+
+
+def replay_envelope(case, protocol, for_apply, verify):
+    """{"code", "inner_code", "failed_op", "op_code"} of one wrapper.json case."""
+    def b(x):
+        return bytes.fromhex(x) if isinstance(x, str) else x
+
+    accounts = {}
+    for a in case["accounts"]:
+        accounts[b(a["id"])] = {"id": b(a["id"]), "thresholds": a["thresholds"],
+                                "signers": [{"type": g["type"], "key": b(g["key"]), "weight": g.get("weight", 1),
+                                             "payload": b(g.get("payload", ""))} for g in a["signers"]]}
+    sigs = [{"hint": b(d["hint"]), "sig": b(d["sig"])} for d in case["sigs"]]
+
+    def check_tx():
+        r = {"code": 0, "inner_code": 0, "failed_op": -1, "op_code": 0}
+        ck = Checker(protocol, b(case["hash"]), sigs, verify)
+        src = accounts.get(b(case["source"]))
+        if src is None:
+            r["code"] = TX_NO_ACCOUNT
+            return r
+        if not ck.check(_signers_of(src), src["thresholds"][1]):
+            r["code"] = TX_BAD_AUTH
+            return r
+        extra = [{"type": g["type"], "key": b(g["key"]), "weight": 1, "payload": b(g.get("payload", ""))}
+                 for g in case.get("extra", [])]
+        if protocol >= 19 and extra and not ck.check(extra, len(extra)):
+            r["code"] = TX_BAD_AUTH
+            return r
+        if for_apply and protocol < 10:
+            return r
+        for i, op in enumerate(case["ops"]):
+            oid = b(op["source"]) if op.get("source") else b(case["source"])
+            acc = accounts.get(oid)
+            if acc is not None:
+                ok, opc = ck.check(_signers_of(acc), acc["thresholds"][op["level"]]), OP_BAD_AUTH
+            elif not op.get("source"):
+                ok, opc = False, OP_NO_ACCOUNT
+            else:
+                ok = ck.check([{"type": ED25519, "key": oid, "weight": 1, "payload": b""}], 0)
+                opc = OP_BAD_AUTH
+            if not ok and r["code"] != TX_FAILED:
+                r.update(code=TX_FAILED, failed_op=i, op_code=opc)
+                if not for_apply:
+                    return r
+        if r["code"] == TX_FAILED:
+            return r
+        if not ck.all_used():
+            r["code"] = TX_BAD_AUTH_EXTRA
+        return r
+
+    fb = case.get("fee_bump")
+    if not fb:
+        return check_tx()
+    r = {"code": 0, "inner_code": 0, "failed_op": -1, "op_code": 0}
+    if protocol < 13:
+        r["code"] = -12
+        return r
+    fee = accounts.get(b(fb["fee_source"]))
+    if fee is None:
+        r["code"] = TX_NO_ACCOUNT
+        return r
+    ck = Checker(protocol, b(fb["hash"]), [{"hint": b(d["hint"]), "sig": b(d["sig"])} for d in fb["sigs"]], verify)
+    if not ck.check(_signers_of(fee), fee["thresholds"][1]):
+        r["code"] = TX_BAD_AUTH
+        return r
+    if not ck.all_used():
+        r["code"] = TX_BAD_AUTH_EXTRA
+        return r
+    inner = check_tx()
+    r.update(code=1 if inner["code"] == 0 else -13, inner_code=inner["code"], failed_op=inner["failed_op"],
+             op_code=inner["op_code"])
+    return r
