@@ -93,6 +93,12 @@ typedef struct svh_engine_stats {
   uint64_t gpu_signatures, gpu_batches, cpu_signatures, fallbacks;
 } svh_engine_stats;
 void svh_engine_counts_ex(svh_engine_stats* out); /* flushes all four */
+/* Batch-size and latency histograms (PubKeyUtils::flushEngineHistograms):
+ * out[0..31] GPU batch sizes, [32..63] GPU latencies (us), [64..95] CPU-path
+ * batch sizes, [96..127] CPU-path latencies; bucket b counts values v with
+ * floor(log2(v)) == b (v = 0 in bucket 0, the last bucket open-ended).
+ * Flushes. */
+void svh_engine_histograms(uint64_t out[128]);
 /* batches with at most max_misses cache misses run on the CPU path (default 1) */
 void svh_set_cpu_threshold(size_t max_misses);
 /* engine-only batch, no cache (PubKeyUtils::verifyBatchUncached) */

@@ -235,12 +235,13 @@ int sv_key_cache_get_stats(int device, sv_key_cache_stats* out);
 
 /* Test knobs (0 in production).  TRIVIAL_PAIR: every lane verifies through the
  * fallback pair (h, 1) of the half-size equation (lattice.h), i.e. the
- * full-length scalar; MAX_WINDOWS: every wave runs all 64 windows; FAIL: every
- * GPU entry point returns SV_ERR_HIP without touching the device (callers'
- * CPU fallback tests); PREP_ONLY (profiling): throughput-path launches run the
- * per-signature prep kernel only (verdicts are NOT written), so kernel-time
- * accounting splits into prep and scalar multiplication.  Returns the previous
- * flags, or SV_ERR_INVALID_ARG. */
+ * full-length scalar; MAX_WINDOWS: every wave runs all 64 windows (both only
+ * select code paths; verdicts are unchanged).  FAIL: every GPU entry point
+ * returns SV_ERR_HIP without touching the device (callers' CPU fallback
+ * tests); PREP_ONLY (profiling): throughput-path launches run the
+ * per-signature prep kernel only (verdicts are NOT written).  FAIL and
+ * PREP_ONLY are refused (SV_ERR_INVALID_ARG) unless the process environment
+ * has SV_TEST_KNOBS=1.  Returns the previous flags, or SV_ERR_INVALID_ARG. */
 #define SV_DBG_TRIVIAL_PAIR 0x1u
 #define SV_DBG_MAX_WINDOWS 0x2u
 #define SV_DBG_FAIL 0x4u

@@ -335,6 +335,30 @@ uint64_t gVerifyCacheHit = 0;
 uint64_t gVerifyCacheMiss = 0;
 uint64_t gBatchId = 0;  // owner ids of pending entries (under the mutex)
 std::atomic<uint64_t> gGpuSigs{0}, gGpuBatches{0}, gCpuSigs{0}, gFallbacks{0};
+// batch-size and latency histograms (log2 buckets), per path
+std::atomic<uint64_t> gHist[4][PubKeyUtils::EngineHistograms::kBuckets];
+
+int log2Bucket(uint64_t v) {
+  int b = 0;
+  while (v > 1 && b + 1 < PubKeyUtils::EngineHistograms::kBuckets) {
+    v >>= 1;
+    ++b;
+  }
+  return b;
+}
+void recordBatch(bool gpu, size_t n, std::chrono::steady_clock::time_point t0) {
+  const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+  gHist[gpu ? 0 : 2][log2Bucket(n)].fetch_add(1, std::memory_order_relaxed);
+  gHist[gpu ? 1 : 3][log2Bucket((uint64_t)(us < 0 ? 0 : us))].fetch_add(1, std::memory_order_relaxed);
+}
+// runs f() (an engine or CPU-path verification of n items) and records it
+template <class F>
+auto timedBatch(bool gpu, size_t n, F&& f) -> decltype(f()) {
+  const auto t0 = std::chrono::steady_clock::now();
+  auto r = f();
+  recordBatch(gpu, n, t0);
+  return r;
+}
 std::atomic<PubKeyUtils::BatchVerifyFn> gTestVerifier{nullptr};
 std::atomic<PubKeyUtils::KeyedBatchVerifyFn> gTestKeyedVerifier{nullptr};
 std::atomic<size_t> gKeyedThreshold{256};
@@ -543,7 +567,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
         walk();
         tC = std::chrono::steady_clock::now();
       };
-    if (gpuVerify(items, rows, verdict.data(), keys.data(), &phase1) == SV_OK) {
+    if (timedBatch(true, E, [&] { return gpuVerify(items, rows, verdict.data(), keys.data(), &phase1); }) == SV_OK) {
       gGpuSigs += E;
       gGpuBatches += 1;
       if (trace) {
@@ -558,7 +582,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
         hostKeys(items, rows, keys.data());
         phase1();
       }
-      cpuVerify(items, rows, verdict.data());
+      timedBatch(false, E, [&] { cpuVerify(items, rows, verdict.data()); return 0; });
     }
     if (!walked) phase1();  // (not reached: the engine ran it on success)
     const auto tE = std::chrono::steady_clock::now();
@@ -613,13 +637,13 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     mv.assign(M, 0);
     if (M > 0) {
       if (M <= gCpuThreshold.load() && gTestVerifier.load() == nullptr) {
-        cpuVerify(items, missItems, mv.data());
-      } else if (gpuVerify(items, missItems, mv.data(), nullptr) == SV_OK) {
+        timedBatch(false, M, [&] { cpuVerify(items, missItems, mv.data()); return 0; });
+      } else if (timedBatch(true, M, [&] { return gpuVerify(items, missItems, mv.data(), nullptr); }) == SV_OK) {
         gGpuSigs += M;
         gGpuBatches += 1;
       } else {
         ++gFallbacks;
-        cpuVerify(items, missItems, mv.data());
+        timedBatch(false, M, [&] { cpuVerify(items, missItems, mv.data()); return 0; });
       }
     }
     // phase 3: fill in the pending values
@@ -639,19 +663,21 @@ void verifyBatchUncached(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   if (n == 0) return;
   BatchVerifyFn tv = gTestVerifier.load();
   if (!tv && n <= gCpuThreshold.load()) {
-    sv_ed25519_verify_batch_cpu(pk, sig, msg, off, len, n, verdict, 0);
+    timedBatch(false, n, [&] { return sv_ed25519_verify_batch_cpu(pk, sig, msg, off, len, n, verdict, 0); });
     gCpuSigs += n;
     return;
   }
-  const int rc = tv ? tv(pk, sig, msg, off, len, n, verdict)
-                    : sv_ed25519_verify_batch(pk, sig, msg, off, len, n, verdict, nullptr);
+  const int rc = timedBatch(true, n, [&] {
+    return tv ? tv(pk, sig, msg, off, len, n, verdict)
+              : sv_ed25519_verify_batch(pk, sig, msg, off, len, n, verdict, nullptr);
+  });
   if (rc == SV_OK) {
     gGpuSigs += n;
     gGpuBatches += 1;
     return;
   }
   ++gFallbacks;
-  sv_ed25519_verify_batch_cpu(pk, sig, msg, off, len, n, verdict, 0);
+  timedBatch(false, n, [&] { return sv_ed25519_verify_batch_cpu(pk, sig, msg, off, len, n, verdict, 0); });
   gCpuSigs += n;
 }
 
@@ -690,6 +716,17 @@ EngineCounts flushEngineCounts() {
   c.cpuSignatures = gCpuSigs.exchange(0);
   c.fallbacks = gFallbacks.exchange(0);
   return c;
+}
+
+EngineHistograms flushEngineHistograms() {
+  EngineHistograms h;
+  for (int b = 0; b < EngineHistograms::kBuckets; ++b) {
+    h.gpuBatchSize[b] = gHist[0][b].exchange(0);
+    h.gpuLatencyUs[b] = gHist[1][b].exchange(0);
+    h.cpuBatchSize[b] = gHist[2][b].exchange(0);
+    h.cpuLatencyUs[b] = gHist[3][b].exchange(0);
+  }
+  return h;
 }
 
 void flushEngineCounts(uint64_t& signatures, uint64_t& batches) {

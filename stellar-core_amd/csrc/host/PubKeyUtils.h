@@ -133,6 +133,18 @@ struct EngineCounts {
 EngineCounts flushEngineCounts();
 void flushEngineCounts(uint64_t& signatures, uint64_t& batches);
 
+// Histograms beside the crypto.verify.{hit,miss,total} meters
+// (/root/reference/docs/metrics.md:48-50): every verification call that
+// reaches the engine (gpu*) or the CPU path (cpu*) is counted by its batch
+// size and its wall latency in microseconds, in bucket b = floor(log2(v))
+// (b = 0 also holds v = 0; the last bucket holds everything above).  Bounded
+// (fixed buckets), lock-free; flushing reads and zeroes them.
+struct EngineHistograms {
+  static constexpr int kBuckets = 32;
+  uint64_t gpuBatchSize[kBuckets], gpuLatencyUs[kBuckets], cpuBatchSize[kBuckets], cpuLatencyUs[kBuckets];
+};
+EngineHistograms flushEngineHistograms();
+
 // Test hook: cache keys currently held, in the cache's insertion-order vector
 // (the reference's mValuePtrs), for replay tests of the eviction policy.
 std::vector<Hash> cacheKeysForTesting();

@@ -156,6 +156,17 @@ void svh_engine_counts_ex(svh_engine_stats* out) {
     out->fallbacks = c.fallbacks;
   }
 }
+void svh_engine_histograms(uint64_t out[4 * 32]) {
+  const auto h = PubKeyUtils::flushEngineHistograms();
+  static_assert(PubKeyUtils::EngineHistograms::kBuckets == 32, "svh_engine_histograms layout");
+  if (!out) return;
+  for (int b = 0; b < 32; ++b) {
+    out[b] = h.gpuBatchSize[b];
+    out[32 + b] = h.gpuLatencyUs[b];
+    out[64 + b] = h.cpuBatchSize[b];
+    out[96 + b] = h.cpuLatencyUs[b];
+  }
+}
 void svh_set_test_verifier(svh_batch_verify_fn fn) { PubKeyUtils::setBatchVerifierForTesting(fn); }
 void svh_set_test_keyed_verifier(svh_keyed_verify_fn fn) { PubKeyUtils::setKeyedBatchVerifierForTesting(fn); }
 void svh_set_keyed_threshold(size_t min_items) { PubKeyUtils::setKeyedBatchThreshold(min_items); }

@@ -1112,6 +1112,13 @@ int check_msgs(const HostIn& in, size_t n) {
   return SV_OK;
 }
 
+// Test-only knobs are enabled by SV_TEST_KNOBS=1 in the process environment
+// (tests/conftest.py, profiling tools); a production process never sets it.
+bool test_knobs_enabled() {
+  const char* v = getenv("SV_TEST_KNOBS");
+  return v && v[0] == '1' && v[1] == 0;
+}
+
 int debug_fail() {
   if (g_dbg.load() & SV_DBG_FAIL) return fail(SV_ERR_HIP, "injected device error (sv_set_debug_flags SV_DBG_FAIL)");
   return SV_OK;
@@ -1407,6 +1414,10 @@ int sv_set_kernel_path(int path) {
 
 int sv_set_debug_flags(uint32_t flags) {
   if (flags & ~(SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_FAIL | SV_DBG_PREP_ONLY)) return SV_ERR_INVALID_ARG;
+  // the knobs that change what a call returns (FAIL: every call errs;
+  // PREP_ONLY: no verdicts) only exist for processes that opt in
+  if ((flags & (SV_DBG_FAIL | SV_DBG_PREP_ONLY)) && !test_knobs_enabled())
+    return fail(SV_ERR_INVALID_ARG, "SV_DBG_FAIL / SV_DBG_PREP_ONLY need SV_TEST_KNOBS=1 in the environment");
   return (int)g_dbg.exchange(flags);
 }
 

@@ -1,18 +1,17 @@
 // gfx950 kernels of the batched ed25519 verification engine.
 //
-// One lane verifies one signature (the per-lane algorithm is verify_core.h).
-// Grid: persistent, gridDim = CUs x resident workgroups per CU; each wave
-// walks the batch in wave-uniform strides of (grid threads), so lanes of a
-// wave always hold 64 consecutive signatures (coalesced SoA loads, one
-// ballot word of the verdict bitmap per wave iteration).
-//
-// Memory per workgroup: a 12 KiB LDS stage per wave for the next table_A entry.
-// Per device: the 2^15+1-entry base-point table (4.7 MB, global, L2/MALL-hot).
-// Memory per lane: a 2304 B slot of the HBM workspace: the signature's 9-entry
-// table of multiples of -A (1728 B) + SV_BATCH_K parked projective points.
-// Lane-major: lanes gather different entries (per-lane digits), so keeping
-// each lane's entry contiguous (192 B) is what bounds the line traffic (a
-// wave-interleaved layout measured ~4x more L2-miss traffic, profiles/r01/).
+//   sv_prep_kernel / sv_main_kernel  the throughput path: one lane per
+//       signature, the half-size equation of lattice.h, per chunk a prep
+//       kernel (hash, checks, decompression, Euclid, tables of -A / -R and
+//       digit records into the chunk workspace) and a persistent main kernel
+//       (the windowed double-scalar multiplication, table entries by LDS-DMA)
+//   sv_octet_kernel  the latency path for keys not in the key cache: one
+//       signature per octet of lanes, every point operation split over a quad
+//       (quad.h); the warm-key kernel is sv_comb.hip
+//   sv_btab_init_kernel  the base-point tables (device init)
+//   sv_sign_kernel   the RFC 8032 signer (benchmark datasets)
+// Kernel variants retired in round 3 are kept, unbuilt, in
+// tools/variants/legacy_kernels.hip.txt.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -55,82 +54,6 @@ __device__ __forceinline__ void sv_load_btab_lds(sv_u4* s_btab, const sv_u4* g_b
   __syncthreads();
 }
 
-// Each wave iteration handles SV_BATCH_K groups of 64 consecutive signatures
-// (group k at base + k*stride); each lane runs steps (1)-(7) for its K
-// signatures, parks the projective results in its workspace slot, then
-// inverts all K Z coordinates with ONE exponentiation (Montgomery's trick)
-// and finishes step (8).  Groups entirely past n are skipped (wave-uniform)
-// and enter the batch inversion as Z = 1.
-template <int MODE>  // 0: fixed 32-byte messages, 1: variable length, 2: fixed other length
-__global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_kernel(sv_kparams p) {
-#if SV_B_BITS == 8
-  __shared__ sv_u4 s_btab[SV_BTAB_ENTRIES * (SV_BTAB_STRIDE / 4)];
-  sv_load_btab_lds(s_btab, p.btab);
-  const sv_u4* btab = s_btab;
-#else
-  const sv_u4* btab = p.btab;  // 4.7 MB, L2/MALL-resident
-#endif
-  __shared__ sv_u4 s_stage[SV_BLOCK / 64][SV_STAGE_QUADS];  // per-wave table_A entry stage
-
-  const uint32_t lane = threadIdx.x & 63u;
-  sv_u4* stage = s_stage[threadIdx.x >> 6];
-  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // lane-major workspace slot: table_A (1728 B) + K pending points
-  sv_u4* slot = p.ws + gtid * SV_SLOT_QUADS;
-  sv_u4* pend = slot + SV_ATAB_ENTRIES * SV_ATAB_QUADS;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-
-  for (uint64_t base = gtid - lane; base < p.n; base += SV_BATCH_K * stride) {
-    uint32_t okmask = 0;
-    int ngroups = 0;
-    SV_NOUNROLL for (int k = 0; k < SV_BATCH_K; ++k) {
-      const uint64_t gbase = base + (uint64_t)k * stride;
-      if (gbase >= p.n) break;  // wave-uniform
-      ngroups = k + 1;
-      const uint64_t i = gbase + lane;
-      const uint64_t ii = i < p.n ? i : p.n - 1;  // idle tail lanes redo the last item
-      uint32_t A[8], S[8], hram[16];
-      sv_load_and_hash<MODE>(p, ii, A, S, hram);
-      ge_p3 P;
-      const bool ok = sv_verify_pre<SV_STAGE_A>(P, A, p.sig + 4 * ii, S, hram, slot, 1, btab, stage);
-      okmask |= (ok ? 1u : 0u) << k;
-      sv_store_fe3(pend + k * SV_PEND_QUADS, 1, P.X);
-      sv_store_fe3(pend + k * SV_PEND_QUADS + 3, 1, P.Y);
-      sv_store_fe3(pend + k * SV_PEND_QUADS + 6, 1, P.Z);
-    }
-    {
-      fe z[SV_BATCH_K], zi[SV_BATCH_K];
-      SV_UNROLL for (int k = 0; k < SV_BATCH_K; ++k) {
-        if (k < ngroups) sv_load_fe3(z[k], pend + k * SV_PEND_QUADS + 6, 1);
-        else fe_1(z[k]);
-      }
-      fe_batch_invert<SV_BATCH_K>(zi, z);
-      SV_UNROLL for (int k = 0; k < SV_BATCH_K; ++k) sv_store_fe3(pend + k * SV_PEND_QUADS + 6, 1, zi[k]);
-    }
-    SV_NOUNROLL for (int k = 0; k < ngroups; ++k) {
-      const uint64_t gbase = base + (uint64_t)k * stride;
-      const uint64_t i = gbase + lane;
-      const bool active = i < p.n;
-      const uint64_t ii = active ? i : p.n - 1;
-      fe X, Y, zi;
-      sv_load_fe3(X, pend + k * SV_PEND_QUADS, 1);
-      sv_load_fe3(Y, pend + k * SV_PEND_QUADS + 3, 1);
-      sv_load_fe3(zi, pend + k * SV_PEND_QUADS + 6, 1);
-      const bool ok = ((okmask >> k) & 1u) && sv_encode_matches(X, Y, zi, p.sig + 4 * ii) && active;
-      if (active) p.verdict[i] = ok ? 1 : 0;
-      const uint64_t mask = __ballot(ok);
-      if (p.bitmap != nullptr && lane == 0) p.bitmap[gbase >> 6] = mask;
-    }
-  }
-}
-
-// Half-size verification (lattice.h): one signature per lane per wave
-// iteration.  Per lane: checks (1)-(5) + decode of R, Euclid reduction of h,
-// tables of -A and -R in the workspace slot; the wave then runs W windows,
-// W = the maximum over its lanes (33 for ~91% of waves, 34 for most others),
-// and each lane accepts iff P' is the identity.  No inversion is needed.
-// SV_PHASE_PROF (developer builds only, tools/phase_prof.py): lane 0 of every
-// wave accumulates s_memtime deltas per phase into sv_phase_cycles.
 #ifdef SV_PHASE_PROF
 __device__ unsigned long long sv_phase_cycles[8];
 #define SV_PHASE(k)                                              \
@@ -142,65 +65,6 @@ __device__ unsigned long long sv_phase_cycles[8];
 #else
 #define SV_PHASE(k) ((void)0)
 #endif
-
-template <int MODE>
-__global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_verify_lat_kernel(sv_kparams p) {
-  __shared__ sv_u4 s_stage[SV_BLOCK / 64][2 * SV_LTAB_QUADS * 64];  // per-wave A and R entry stage
-  const uint32_t lane = threadIdx.x & 63u;
-  sv_u4* stage = s_stage[threadIdx.x >> 6];
-  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  sv_u4* tabA = p.ws + gtid * SV_SLOT_QUADS;
-  sv_u4* tabR = tabA + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
-  const sv_u4* btab0 = p.btab;
-  const sv_u4* btab1 = p.btab + SV_LBTAB_ENTRIES * SV_BTAB_QUADS;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-
-  for (uint64_t base = gtid - lane; base < p.n; base += stride) {
-    const uint64_t i = base + lane;
-    const bool active = i < p.n;
-    const uint64_t ii = active ? i : p.n - 1;  // idle tail lanes redo the last item
-#ifdef SV_PHASE_PROF
-    unsigned long long t_prev = __builtin_amdgcn_s_memtime();
-#endif
-    uint32_t A[8], S[8], hram[16], R[8];
-    sv_load_and_hash<MODE>(p, ii, A, S, hram);
-    sv_unpack2(R, p.sig + 4 * ii);
-    SV_PHASE(0);
-    sv_lat lat;
-#ifdef SV_PHASE_PROF
-    bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
-              sv_point_canonical(R);
-    ge_p3 negA, negR;
-    ok = ge_frombytes(negA, A, true) && ok;
-    ok = ge_frombytes(negR, R, true) && ok;
-    SV_PHASE(1);
-    {
-      uint32_t h[8];
-      sc_reduce512(h, hram);
-      sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
-    }
-    SV_PHASE(2);
-    sv_build_ltab(tabA, negA);
-    sv_build_ltab(tabR, negR);
-    SV_PHASE(3);
-#else
-    bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
-#endif
-    const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
-    sv_lat_digits D;
-    sv_lat_prepare(D, lat, S, W);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // table stores before the DMA reads
-    SV_PHASE(4);
-    ge_p3 P;
-    sv_lat_scalarmult<true>(P, D, W, tabA, tabR, btab0, btab1, stage);
-    SV_PHASE(5);
-    ok = ok && sv_is_identity(P) && active;
-    SV_PHASE(6);
-    if (active) p.verdict[i] = ok ? 1 : 0;
-    const uint64_t mask = __ballot(ok);
-    if (p.bitmap != nullptr && lane == 0) p.bitmap[base >> 6] = mask;
-  }
-}
 
 // ---------------------------------------------- split form (SV_SPLIT = 1)
 // The per-signature phases (SHA-512, checks, decompression, mod L, Euclid,
@@ -468,17 +332,8 @@ __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cpa
 }
 
 // ------------------------------------------- latency path (quad.h)
-// One signature per quad of lanes, 16 signatures per single-wave workgroup.
-// Per quad: every lane hashes and reduces (redundantly, so all four hold the
-// digits); lanes of even role decompress A, odd roles R; roles 0 / 1 build
-// table_A / table_R into the workgroup's LDS; then the windowed scalar
-// multiplication runs with every point operation split over the quad.
-// Verdict bytes by role-0 lanes; the bitmap as one 16-bit store per workgroup
-// (bits 16 k .. 16 k + 15 of word k / 4).
-#ifndef SV_LAT_OCTET
-#define SV_LAT_OCTET 1
-#endif
-#define SV_QSIGS 16
+// Helpers of the octet kernel below (every point operation split over a quad
+// of lanes).
 #define SV_QENT_DW 40  // cached entry: YpX, YmX, Z, T2d x 10 dwords
 
 // this lane's operand of cached entry e (LDS): role 0 T2d, role 1 Z, roles
@@ -500,109 +355,8 @@ __device__ __forceinline__ void qd_load_affine(fe& o, const sv_u4* ent, uint32_t
   if (role == 1) fe_1(o);
 }
 
-template <int MODE>
-__global__ __launch_bounds__(64, 1) void sv_quick_kernel(sv_kparams p) {
-  __shared__ uint32_t s_tab[SV_QSIGS][2][SV_ATAB_ENTRIES][SV_QENT_DW];  // 46 KB
-  const uint32_t lane = threadIdx.x;
-  const uint32_t role = lane & 3u, sl = lane >> 2;
-  const qd_role q{role == 1, role == 2, role == 3};
-  const uint64_t i = (uint64_t)blockIdx.x * SV_QSIGS + sl;
-  const bool active = i < p.n;
-  const uint64_t ii = active ? i : p.n - 1;  // idle tail quads redo the last item
-  uint32_t A[8], S[8], hram[16], R[8];
-  sv_load_and_hash<MODE>(p, ii, A, S, hram);
-  sv_unpack2(R, p.sig + 4 * ii);
-  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
-            sv_point_canonical(R);
-#ifndef SV_QPROF_NODEC  // (developer A/B builds only: phase timing of this kernel)
-  {
-    // decompress: even roles -A, odd roles -R; roles 0 / 1 keep their table
-    uint32_t E[8];
-    SV_UNROLL for (int k = 0; k < 8; ++k) E[k] = (role & 1u) ? R[k] : A[k];
-    ge_p3 Pt;
-    const uint32_t dok = ge_frombytes(Pt, E, true) ? 1u : 0u;
-    ok = ok && (qd_from<0>(dok) & qd_from<1>(dok)) != 0;
-    ge_cached c1, ce;
-    ge_p3_to_cached(c1, Pt);
-    ge_cached_identity(ce);
-    uint32_t* tab = &s_tab[sl][role & 1u][0][0];
-    const bool store = role < 2;
-    if (store) sv_store_lentry((sv_u4*)tab, ce);
-    if (store) sv_store_lentry((sv_u4*)(tab + SV_QENT_DW), c1);
-    ge_p3 P3 = Pt;
-    ge_p1p1 Qa;
-    SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
-      ge_add_preswapped(Qa, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, false);
-      ge_p1p1_to_p3(P3, Qa);
-      ge_p3_to_cached(ce, P3);
-      if (store) sv_store_lentry((sv_u4*)(tab + e * SV_QENT_DW), ce);
-    }
-  }
-#endif
-  sv_lat lat;
-  {
-    uint32_t h[8];
-    sc_reduce512(h, hram);
-    sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
-  }
-#ifdef SV_QPROF_NOMUL
-  const int W = 0;
-#else
-  const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
-#endif
-  sv_lat_digits D;
-  sv_lat_prepare(D, lat, S, W);
-  __syncthreads();  // tables visible to the whole quad
-
-  const sv_u4* btab0 = p.btab;
-  const sv_u4* btab1 = p.btab + SV_LBTAB_ENTRIES * SV_BTAB_QUADS;
-  const uint32_t* tabA = &s_tab[sl][0][0][0];
-  const uint32_t* tabR = &s_tab[sl][1][0][0];
-  ge_p3 P;
-  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
-  SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
-    int32_t dA = sc_pop_top(D.dA, 4);
-    int32_t dR = sc_pop_top(D.dR, 4);
-    if (w == W - 1) {
-      if (D.top8A) dA = 8;
-      if (D.top8R) dR = 8;
-    }
-    if (D.rneg) dR = -dR;
-    int32_t dB0, dB1;
-    fe b0, b1;
-    const bool bwin = sv_lat_bdigits(D, w, dB0, dB1);
-    if (bwin) {
-      // issued before the doublings: the loads land while they run
-      qd_load_affine(b0, btab0 + (dB0 < 0 ? -dB0 : dB0) * SV_BTAB_QUADS, role, dB0 < 0);
-      qd_load_affine(b1, btab1 + (dB1 < 0 ? -dB1 : dB1) * SV_BTAB_QUADS, role, dB1 < 0);
-    }
-    if (w != W - 1) {
-      SV_NOUNROLL for (int k = 0; k < 4; ++k) qd_dbl(P, q, k == 3);
-    }
-    fe m;
-    qd_load_cached(m, tabA + (dA < 0 ? -dA : dA) * SV_QENT_DW, role, dA < 0);
-    qd_add(P, m, q, dA < 0, true);
-    qd_load_cached(m, tabR + (dR < 0 ? -dR : dR) * SV_QENT_DW, role, dR < 0);
-    qd_add(P, m, q, dR < 0, bwin);
-    if (bwin) {
-      qd_add(P, b0, q, dB0 < 0, true);
-      qd_add(P, b1, q, dB1 < 0, false);
-    }
-  }
-  ok = ok && sv_is_identity(P);
-  if (active && role == 0) p.verdict[i] = ok ? 1 : 0;
-  const uint64_t bal = __ballot(ok && active && role == 0);
-  if (p.bitmap != nullptr && lane == 0) {
-    uint16_t m16 = 0;
-    SV_UNROLL for (int k = 0; k < SV_QSIGS; ++k) m16 |= (uint16_t)(((bal >> (4 * k)) & 1u) << k);
-    ((uint16_t*)p.bitmap)[blockIdx.x] = m16;
-    if (blockIdx.x == gridDim.x - 1)  // (bits past n read as 0, as on the throughput path)
-      for (uint32_t b = blockIdx.x + 1; b % 4 != 0; ++b) ((uint16_t*)p.bitmap)[b] = 0;
-  }
-}
-
 // ------------------------------------------- latency path, two quads per signature
-// (SV_LAT_OCTET, default) One signature per OCTET of lanes: the two quads of
+// One signature per OCTET of lanes: the two quads of
 // the octet evaluate the two halves of (*) in lattice.h in parallel,
 //   quad 0:  P_A = [c0](-A) + [s_lo] B           (table_A, e B)
 //   quad 1:  P_R = [c1](-R) + [s_hi] 2^128 B     (table_R, e 2^128 B)
@@ -795,7 +549,9 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
   ok = ok && s_dok[sl] != 0;
 #endif
 
+#if !SV_LAT_BOFF_ON
   const sv_u4* btab = p.btab + (half ? SV_LBTAB_ENTRIES * SV_BTAB_QUADS : 0);
+#endif
   const uint32_t* tab = &s_tab[sl][half][0][0];
   // this quad's digit string and its top-digit carry
   uint32_t dg[8];
@@ -1102,20 +858,7 @@ int sv_occupancy_blocks_per_cu(void) {
   (void)b2;
   return ms < 1 ? 1 : ms;
 #else
-#if SV_LATTICE
-#define SV_VK sv_verify_lat_kernel
-#else
-#define SV_VK sv_verify_kernel
-#endif
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, SV_VK<0>, SV_BLOCK, 0) != hipSuccess) b0 = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b1, SV_VK<1>, SV_BLOCK, 0) != hipSuccess) b1 = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b2, SV_VK<2>, SV_BLOCK, 0) != hipSuccess) b2 = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b3, sv_sign_kernel, SV_BLOCK, 0) != hipSuccess) b3 = 1;
-  int m = b0;
-  if (b1 > m) m = b1;
-  if (b2 > m) m = b2;
-  if (b3 > m) m = b3;
-  return m < 1 ? 1 : m;
+#error "the product build is the split half-size path (SV_LATTICE = SV_SPLIT = 1)"
 #endif
 }
 
@@ -1138,7 +881,6 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
   p.dbg = dbg;
 #if SV_LATTICE
   if (path == 2) {  // SV_PATH_LATENCY
-#if SV_LAT_OCTET
     const unsigned og = (unsigned)((n + SV_OSIGS - 1) / SV_OSIGS);
     if (mode == 0)
       hipLaunchKernelGGL(sv_octet_kernel<0>, dim3(og), dim3(SV_OCTET_BLOCK), 0, s, p);
@@ -1146,15 +888,6 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
       hipLaunchKernelGGL(sv_octet_kernel<1>, dim3(og), dim3(SV_OCTET_BLOCK), 0, s, p);
     else
       hipLaunchKernelGGL(sv_octet_kernel<2>, dim3(og), dim3(SV_OCTET_BLOCK), 0, s, p);
-#else
-    const unsigned qg = (unsigned)((n + SV_QSIGS - 1) / SV_QSIGS);
-    if (mode == 0)
-      hipLaunchKernelGGL(sv_quick_kernel<0>, dim3(qg), dim3(64), 0, s, p);
-    else if (mode == 1)
-      hipLaunchKernelGGL(sv_quick_kernel<1>, dim3(qg), dim3(64), 0, s, p);
-    else
-      hipLaunchKernelGGL(sv_quick_kernel<2>, dim3(qg), dim3(64), 0, s, p);
-#endif
     return hipGetLastError();
   }
 #endif
@@ -1180,20 +913,8 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
       hipLaunchKernelGGL(sv_prep_kernel<2>, dim3(pg), dim3(SV_BLOCK), 0, s, c);
     if (!(dbg & SV_DBG_PREP_ONLY)) hipLaunchKernelGGL(sv_main_kernel, dim3(grid < pg ? grid : pg), dim3(SV_BLOCK), 0, s, c);
   }
-#elif SV_LATTICE
-  if (mode == 0)
-    hipLaunchKernelGGL(sv_verify_lat_kernel<0>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
-  else if (mode == 1)
-    hipLaunchKernelGGL(sv_verify_lat_kernel<1>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
-  else
-    hipLaunchKernelGGL(sv_verify_lat_kernel<2>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
 #else
-  if (mode == 0)
-    hipLaunchKernelGGL(sv_verify_kernel<0>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
-  else if (mode == 1)
-    hipLaunchKernelGGL(sv_verify_kernel<1>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
-  else
-    hipLaunchKernelGGL(sv_verify_kernel<2>, dim3(grid), dim3(SV_BLOCK), 0, s, p);
+#error "the product build is the split half-size path (SV_LATTICE = SV_SPLIT = 1)"
 #endif
   return hipGetLastError();
 }

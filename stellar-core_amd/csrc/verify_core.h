@@ -52,11 +52,8 @@ struct __attribute__((aligned(16))) sv_u4 {
 // a negative digit swaps needs the 3-quad padding).
 #define SV_ATAB_ENTRIES 9
 #define SV_ATAB_QUADS 11
-// Signatures per lane whose final inversions are batched (Montgomery trick),
-// and the per-lane workspace slot: table_A + K pending points (X, Y, Z).
-#define SV_BATCH_K 4
-#define SV_PEND_QUADS 9
-#define SV_SLOT_QUADS_W (SV_ATAB_ENTRIES * SV_ATAB_QUADS + SV_BATCH_K * SV_PEND_QUADS)
+// Per-lane workspace slot of the signer (sv_sign_kernel): its table_A.
+#define SV_SLOT_QUADS_W (SV_ATAB_ENTRIES * SV_ATAB_QUADS)
 // Half-size path (lattice.h): tables of -A and -R, 9 entries x 10 quads each
 // (YpX, YmX, Z, T2d as 4 x 10 dwords back to back; a negative digit swaps
 // YpX/YmX by select after the load).
@@ -346,22 +343,6 @@ SV_HD bool sv_verify_core(const uint32_t A[8], const sv_u4* Rp, const uint32_t S
   fe zi;
   fe_invert(zi, P.Z);
   return sv_encode_matches(P.X, P.Y, zi, Rp) && ok;
-}
-
-// Montgomery's simultaneous inversion: zi[k] = 1/z[k] for K field elements
-// with one exponentiation and 3(K-1) multiplications (every z[k] != 0).
-template <int K>
-SV_HD void fe_batch_invert(fe zi[K], const fe z[K]) {
-  fe c[K];
-  c[0] = z[0];
-  SV_UNROLL for (int k = 1; k < K; ++k) fe_mul(c[k], c[k - 1], z[k]);
-  fe inv;
-  fe_invert(inv, c[K - 1]);
-  SV_UNROLL for (int k = K - 1; k > 0; --k) {
-    fe_mul(zi[k], inv, c[k - 1]);
-    fe_mul(inv, inv, z[k]);
-  }
-  zi[0] = inv;
 }
 
 // Base-point table entry e = e·B in affine precomp form (used at init).

@@ -19,6 +19,10 @@ import sys
 import numpy as np
 import pytest
 
+# the engine's error-injection knob (sv_set_debug_flags SV_DBG_FAIL) is
+# refused unless the process opts in (include/stellar_sigverify.h)
+os.environ["SV_TEST_KNOBS"] = "1"
+
 # SIGUSR1 dumps every thread's Python stack (diagnosing a run that does not exit)
 faulthandler.register(signal.SIGUSR1, all_threads=True)
 

@@ -50,6 +50,27 @@ static void lat_need_btab(const sv_lat_digits& D) {
 
 static void load_words(uint32_t w[8], const uint8_t* b) { memcpy(w, b, 32); }
 
+// Signatures whose final inversions share one exponentiation in the grouped
+// host verifier below (the full-length equation; test infrastructure).
+#define SV_BATCH_K 4
+// Montgomery's simultaneous inversion: zi[k] = 1/z[k] for K field elements
+// with one exponentiation and 3(K-1) multiplications (every z[k] != 0).
+template <int K>
+SV_HD void fe_batch_invert(fe zi[K], const fe z[K]) {
+  fe c[K];
+  c[0] = z[0];
+  SV_UNROLL for (int k = 1; k < K; ++k) fe_mul(c[k], c[k - 1], z[k]);
+  fe inv;
+  fe_invert(inv, c[K - 1]);
+  SV_UNROLL for (int k = K - 1; k > 0; --k) {
+    fe_mul(zi[k], inv, c[k - 1]);
+    fe_mul(inv, inv, z[k]);
+  }
+  zi[0] = inv;
+}
+
+
+
 extern "C" {
 
 // field ops on 32-byte little-endian values (value < 2^255 as input)

@@ -6,6 +6,7 @@ import glob
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -101,3 +102,21 @@ def test_kernel_path_setter_validates(sv):
     assert sv.set_kernel_path(prev) == sv.PATH_THROUGHPUT
     with pytest.raises(sv.SigVerifyError):
         sv.set_kernel_path(7)
+
+
+def test_result_changing_knobs_need_opt_in(sv):
+    """SV_DBG_FAIL / SV_DBG_PREP_ONLY (calls that err or write no verdicts) are
+    refused in a process without SV_TEST_KNOBS=1; the path-selecting knobs are
+    not.  Run in a child process: this one opted in (conftest.py)."""
+    code = ("import ctypes,sys; l=ctypes.CDLL(sys.argv[1]); l.sv_set_debug_flags.argtypes=[ctypes.c_uint32];"
+            "print(l.sv_set_debug_flags(4), l.sv_set_debug_flags(8), l.sv_set_debug_flags(1), l.sv_set_debug_flags(0))")
+    env = {k: v for k, v in os.environ.items() if k != "SV_TEST_KNOBS"}
+    env["SV_NO_TORCH"] = "1"
+    out = subprocess.run([sys.executable, "-c", code, sv.LIB_PATH], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["-1", "-1", "0", "1"]
+    env["SV_TEST_KNOBS"] = "1"
+    out = subprocess.run([sys.executable, "-c", code, sv.LIB_PATH], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.stdout.split() == ["0", "4", "8", "1"]

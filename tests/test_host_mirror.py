@@ -204,6 +204,33 @@ def test_cache_cleared_during_batch(host, oracle, golden):
         host.svh_cache_clear()
 
 
+def test_engine_histograms(host, engine, golden):
+    """Batch-size / latency histograms beside the crypto.verify.* counters
+    (docs/metrics.md:48-50): one bucket count per engine call, log2 buckets,
+    flushed on read."""
+    host.svh_engine_histograms.argtypes = [ctypes.c_void_p]
+    h = np.zeros(128, np.uint64)
+    host.svh_engine_histograms(h.ctypes.data)  # (flush earlier tests)
+    d = golden["valid"]
+    for n, start in ((1, 0), (3, 10), (300, 100)):
+        rows = np.arange(n) + start
+        pk, sig = np.ascontiguousarray(d["pk"][rows]), np.ascontiguousarray(d["sig"][rows])
+        off, ln = np.ascontiguousarray(d["msg_off"][rows]), np.ascontiguousarray(d["msg_len"][rows])
+        msg = np.ascontiguousarray(d["msg"])
+        out = np.zeros(n, np.uint8)
+        vp = ctypes.c_void_p
+        assert host.svh_verify_sig_batch(vp(pk.ctypes.data), vp(sig.ctypes.data), None, vp(msg.ctypes.data),
+                                         vp(off.ctypes.data), vp(ln.ctypes.data), ctypes.c_size_t(n),
+                                         vp(out.ctypes.data)) == 0
+        assert out.all()
+    host.svh_engine_histograms(h.ctypes.data)
+    gpu_size, gpu_lat = h[0:32], h[32:64]
+    assert gpu_size[0] == 1 and gpu_size[1] == 1 and gpu_size[8] == 1  # sizes 1, 3, 300
+    assert int(gpu_size.sum()) == 3 == int(gpu_lat.sum()) == engine.calls
+    host.svh_engine_histograms(h.ctypes.data)
+    assert int(h.sum()) == 0  # flushed
+
+
 def test_verify_sig_batch_keyed_path(host, oracle, golden):
     """f4: with the keyed pass (verdicts + cache keys from the engine, no host
     hashing) verdicts, hit/miss counters and cache contents match the hashed

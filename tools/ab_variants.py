@@ -3,6 +3,8 @@
 tools/build_variants.sh).  One 2^20 fixed-32B batch signed on the GPU (1/8 of
 the rows corrupted); every variant must reproduce the baseline's verdicts;
 prints kernel ms per launch (median over interleaved rounds) per variant."""
+import os
+os.environ.setdefault("SV_TEST_KNOBS", "1")  # (sv_set_debug_flags PREP_ONLY / FAIL)
 import ctypes
 import glob
 import os

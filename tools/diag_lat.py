@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Developer tool: latency-path verdicts of one library build against the golden
 fixtures under every debug mode.  Usage: python tools/diag_lat.py [lib.so]"""
+import os
+os.environ.setdefault("SV_TEST_KNOBS", "1")  # (sv_set_debug_flags PREP_ONLY / FAIL)
 import importlib
 import os
 import sys
