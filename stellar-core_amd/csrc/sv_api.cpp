@@ -134,19 +134,23 @@ struct DevBuf {
   }
 };
 
-// Pinned host staging (hipHostMalloc).
+// Pinned host staging (hipHostMalloc).  `mapped` buffers are fine-grained
+// (coherent) and read / written by kernels in place: `dp` is their device
+// address.
 struct HostBuf {
   void* p = nullptr;
+  void* dp = nullptr;
   size_t cap = 0;
+  bool mapped = false;
   int ensure(size_t bytes) {
     if (bytes <= cap) return SV_OK;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
+    release();
     const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 16);
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    hipError_t e =
+        hipHostMalloc(&p, want, mapped ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault);
+    if (e == hipSuccess && mapped) e = hipHostGetDevicePointer(&dp, p, 0);
     if (e != hipSuccess) {
-      p = nullptr;
+      release();
       return fail(SV_ERR_ALLOC, std::string("hipHostMalloc: ") + hipGetErrorString(e));
     }
     cap = want;
@@ -154,7 +158,7 @@ struct HostBuf {
   }
   void release() {
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dp = nullptr;
     cap = 0;
   }
 };
@@ -183,6 +187,7 @@ struct LatLane {
   hipStream_t build = nullptr;   // key-table builds (lowest priority)
   hipEvent_t ev_lat = nullptr, done = nullptr, keys_down = nullptr;
   HostBuf h_in, h_out, h_build;
+  HostBuf z_out;  // mapped: the kernels write verdicts in place
   DevBuf d_in, d_out, d_keys, d_build;
   void* ctab = nullptr;  // tables of B (built at lane init)
   DevBuf ktab, kstat;    // tables of -A per cached key, status per slot
@@ -715,6 +720,7 @@ void release_lat(LatLane& L) {
   L.pending.clear();
   L.pending_n.clear();
   L.h_in.release(); L.h_out.release(); L.h_build.release();
+  L.z_out.release();
   L.d_in.release(); L.d_out.release(); L.d_keys.release(); L.d_build.release();
   L.ktab.release(); L.kstat.release();
   if (L.ctab) (void)hipFree(L.ctab);
@@ -745,6 +751,7 @@ int lat_ready(Device& D) {
   int least = 0, greatest = 0;
   SV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   SV_HIP(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, greatest));
+  L.z_out.mapped = true;
   L.ready = true;  // (release_lat cleans up whatever exists from here on)
   hipError_t e = hipStreamCreateWithPriority(&L.build, hipStreamNonBlocking, least);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.ev_lat, hipEventDisableTiming);
@@ -917,6 +924,23 @@ void lat_build(LatLane& L) {
   L.inflight.push_back(std::move(b));
 }
 
+// Zero-copy verdicts (SV_LAT_ZERO_COPY, default on): the kernel of a
+// verdict-only latency batch writes its verdicts straight into mapped pinned
+// memory, which saves the blit dispatch of a D2H copy (~6 us of a ~0.12 ms
+// batch, tools/gpu/api_probe.hip).  The input image still goes up by one H2D
+// copy: kernels reading it in place over the fabric ran ~11 us longer.
+
+std::atomic<int> g_lat_zc{-1};
+bool lat_zero_copy() {
+  int v = g_lat_zc.load();
+  if (v < 0) {
+    const char* e = getenv("SV_LAT_ZERO_COPY");
+    v = (e && e[0] == '0') ? 0 : 1;
+    g_lat_zc.store(v);
+  }
+  return v != 0;
+}
+
 std::atomic<int> g_lat_trace{-1};
 bool lat_trace() {
   int v = g_lat_trace.load();
@@ -946,20 +970,28 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   const size_t o_ks = (im.bytes + 3) & ~(size_t)3;
   const size_t in_bytes = warm ? o_ks + 4 * n : im.bytes;
   const size_t out_per = (verdict ? 1 : 0) + (keys ? 32 : 0);
-  if ((rc = L.h_in.ensure(in_bytes)) || (rc = L.d_in.ensure(in_bytes)) || (rc = L.h_out.ensure(out_per * n)))
-    return rc;
-  if (verdict && (rc = L.d_out.ensure(n))) return rc;
-  if (keys && (rc = L.d_keys.ensure(32 * n))) return rc;
+  const bool zc = verdict && !keys && lat_zero_copy();
+  if ((rc = L.h_in.ensure(in_bytes)) || (rc = L.d_in.ensure(in_bytes))) return rc;
+  if (zc) {
+    if ((rc = L.z_out.ensure(n))) return rc;
+  } else {
+    if ((rc = L.h_out.ensure(out_per * n))) return rc;
+    if (verdict && (rc = L.d_out.ensure(n))) return rc;
+    if (keys && (rc = L.d_keys.ensure(32 * n))) return rc;
+  }
   uint8_t* h = (uint8_t*)L.h_in.p;
   pack(in, 0, n, im, h);
   if (warm) std::memcpy(h + o_ks, L.kslots.data(), 4 * n);
   const auto t1 = std::chrono::steady_clock::now();
   SV_HIP(hipMemcpyAsync(L.d_in.p, h, in_bytes, hipMemcpyHostToDevice, L.stream));
+  const auto t_up = std::chrono::steady_clock::now();
   uint8_t* d = (uint8_t*)L.d_in.p;
+  void* d_verdict = zc ? L.z_out.dp : L.d_out.p;
   const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
   const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
   uint8_t* ho = (uint8_t*)L.h_out.p;
   const bool early = keys_cb && keys && verdict;
+  auto t_k = t_up;
   if (keys) {
     SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n, L.d_keys.p,
                           L.stream));
@@ -974,17 +1006,19 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
     if ((rc = lat_timing_begin(L, &e0))) return rc;
     if (warm)
       SV_HIP(sv_launch_comb(mode, sv_comb_spw(n, D.cus), d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
-                            L.d_out.p, (const uint32_t*)(d + o_ks), (const uint32_t*)L.ktab.p,
+                            d_verdict, (const uint32_t*)(d + o_ks), (const uint32_t*)L.ktab.p,
                             (const uint32_t*)L.kstat.p, (const uint32_t*)L.ctab, L.stream));
     else
       SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
-                              L.d_out.p, nullptr, nullptr, D.btab, dbg, L.stream));
+                              d_verdict, nullptr, nullptr, D.btab, dbg, L.stream));
     if ((rc = lat_timing_end(L, e0, n))) return rc;
-    SV_HIP(hipMemcpyAsync(ho, L.d_out.p, n, hipMemcpyDeviceToHost, L.stream));
+    t_k = std::chrono::steady_clock::now();
+    if (!zc) SV_HIP(hipMemcpyAsync(ho, L.d_out.p, n, hipMemcpyDeviceToHost, L.stream));
   }
   if (keys && !early)
     SV_HIP(hipMemcpyAsync(ho + (verdict ? n : 0), L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, L.stream));
   SV_HIP(hipEventRecord(L.done, L.stream));
+  const auto t_down = std::chrono::steady_clock::now();
   if (early) {
     SV_HIP(hipEventSynchronize(L.keys_down));
     std::memcpy(keys, ho + n, 32 * n);
@@ -992,16 +1026,22 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
     *cb_done = true;
   }
   lat_build(L);  // (after the verify work: a build waits for it on the device)
+  const auto t_b = std::chrono::steady_clock::now();
   SV_HIP(hipEventSynchronize(L.done));
-  if (verdict) std::memcpy(verdict, ho, n);
+  if (verdict) std::memcpy(verdict, zc ? (const uint8_t*)L.z_out.p : ho, n);
   if (keys && !early) std::memcpy(keys, ho + (verdict ? n : 0), 32 * n);
   if (warm) ++L.warm;
   else ++L.cold;
   if (lat_trace()) {
     const auto t2 = std::chrono::steady_clock::now();
-    fprintf(stderr, "SV_LAT_TRACE n=%zu %s plan+pack %.1f us device %.1f us\n", n, warm ? "warm" : "cold",
-            std::chrono::duration<double, std::micro>(t1 - t0).count(),
-            std::chrono::duration<double, std::micro>(t2 - t1).count());
+    auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::micro>(b - a).count();
+    };
+    fprintf(stderr,
+            "SV_LAT_TRACE n=%zu %s plan+pack %.1f us | h2d call %.1f launch %.1f d2h+rec %.1f build %.1f sync %.1f"
+            " | device %.1f us\n",
+            n, warm ? "warm" : "cold", us(t0, t1), us(t1, t_up), us(t_up, t_k), us(t_k, t_down), us(t_down, t_b),
+            us(t_b, t2), us(t1, t2));
   }
   return SV_OK;
 }
