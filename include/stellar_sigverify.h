@@ -230,6 +230,10 @@ typedef struct sv_key_cache_stats {
   uint64_t cold_batches; /* latency-lane batches served by the octet kernel */
   uint64_t keys_built;   /* key-table builds queued */
   uint64_t evictions;
+  uint64_t shared_launches; /* bulk (throughput-path) launches that ran in shared
+                               mode because latency batches were live: they leave
+                               one workgroup slot per CU to the latency lane
+                               (window SV_LAT_SHARE_MS, default 1000; 0: off) */
 } sv_key_cache_stats;
 int sv_key_cache_get_stats(int device, sv_key_cache_stats* out);
 

@@ -82,7 +82,7 @@ class sv_opts(ctypes.Structure):
 
 class KeyCacheStats(ctypes.Structure):
     _fields_ = [(f, ctypes.c_uint64) for f in ("capacity", "keys", "warm_batches", "cold_batches", "keys_built",
-                                                "evictions")]
+                                                "evictions", "shared_launches")]
 
 
 _lib: Optional[ctypes.CDLL] = None

@@ -464,7 +464,29 @@ SV_HD void fe_sq_cm(fe& h, const fe& f) {
 #define SV_FE_ASM_ON 0
 #endif
 
+// Measurement builds only (-DSV_MADCOUNT; tools/madcount.py): each field
+// product adds its v_mad_u64_u32 count to a device counter once per wave (by
+// the wave's first active lane), so the counter holds the multiply-adds the
+// SIMDs issue.  Counts per generated statement (fe_asm_gen.h; checked by
+// tests/test_host_arith.py): products 101 (100 + the x19 wrap of the top
+// column), squarings 56.
+#define SV_MADS_MUL 101
+#define SV_MADS_SQ 56
+#if defined(SV_MADCOUNT) && defined(__HIPCC__)
+static __device__ unsigned long long sv_madcount[1];
+#endif
+#if defined(SV_MADCOUNT) && defined(__HIP_DEVICE_COMPILE__)
+#define SV_MADS(k)                                                                    \
+  do {                                                                                \
+    if (__lane_id() == (uint32_t)__builtin_amdgcn_readfirstlane((int)__lane_id())) \
+      atomicAdd(&sv_madcount[0], (unsigned long long)(k));                            \
+  } while (0)
+#else
+#define SV_MADS(k) ((void)0)
+#endif
+
 SV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
+  SV_MADS(SV_MADS_MUL);
 #if SV_FE_ASM_ON
   fe_mul_asm(h, f, g);
 #elif SV_COLMAJOR
@@ -482,6 +504,7 @@ SV_HD void fe_premul19(fe19& t, const fe& g) {
 // h = f g with t = fe_premul19(g) (same value and bounds as fe_mul)
 SV_HD void fe_mul_g19(fe& h, const fe& f, const fe& g, const fe19& t) {
 #if SV_FE_ASM_ON
+  SV_MADS(SV_MADS_MUL);
   fe_mul_g19_asm(h, f, g, t);
 #else
   (void)t;
@@ -492,6 +515,7 @@ SV_HD void fe_mul_g19(fe& h, const fe& f, const fe& g, const fe19& t) {
 }
 // h = 2 f g (doubling folded into the operand; inputs must be <= R)
 SV_HD void fe_mul2(fe& h, const fe& f, const fe& g) {
+  SV_MADS(SV_MADS_MUL);
 #if SV_FE_ASM_ON
   fe_mul2_asm(h, f, g);
 #elif SV_COLMAJOR
@@ -504,6 +528,7 @@ SV_HD void fe_mul2(fe& h, const fe& f, const fe& g) {
   SV_FENCE();
 }
 SV_HD void fe_sq(fe& h, const fe& f) {
+  SV_MADS(SV_MADS_SQ);
 #if SV_FE_ASM_ON
   fe_sq_asm(h, f);
 #elif SV_COLMAJOR
@@ -517,6 +542,7 @@ SV_HD void fe_sq(fe& h, const fe& f) {
 }
 // h = 2 f^2 (input must be <= R)
 SV_HD void fe_sq2(fe& h, const fe& f) {
+  SV_MADS(SV_MADS_SQ);
 #if SV_FE_ASM_ON
   fe_sq2_asm(h, f);
 #elif SV_COLMAJOR

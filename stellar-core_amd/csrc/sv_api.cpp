@@ -59,7 +59,9 @@ hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s);
 int sv_occupancy_blocks_per_cu(void);
 hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, const void* sig, const void* msg,
                             const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n,
-                            void* verdict, void* bitmap, void* ws, const void* btab, uint32_t dbg, hipStream_t s);
+                            void* verdict, void* bitmap, void* ws, const void* btab, uint32_t dbg, int share,
+                            hipStream_t s);
+int sv_share_blocks_per_cu(void);
 hipError_t sv_launch_sign(unsigned grid, const void* seed, const void* msg, uint64_t n, void* pk, void* sig,
                           void* ws, const void* btab, hipStream_t s);
 hipError_t sv_launch_hash(int kind, unsigned max_blocks, const void* pk, const void* sig, const void* msg,
@@ -217,6 +219,7 @@ struct Device {
   bool ready = false;  // resources created lazily on first use (under mu)
   int cus = 0;
   unsigned grid = 0;  // persistent grid (workgroups)
+  unsigned grid_share = 0;  // the same in shared mode (latency batches live: share_now)
   hipStream_t stream = nullptr, h2d = nullptr, d2h = nullptr;
   void* btab = nullptr;
   DevBuf ws;  // kernel workspace, grown on demand (after draining `stream`)
@@ -231,6 +234,8 @@ struct Device {
   double total_ms = 0;
   uint64_t launches = 0, sigs = 0;
   LatLane lat;
+  std::atomic<int64_t> lat_last_ns{INT64_MIN / 2};  // steady clock of the last latency-lane batch
+  std::atomic<uint64_t> shared_launches{0};          // bulk launches in shared mode
 };
 
 std::mutex g_mu;
@@ -303,6 +308,7 @@ int init_device(Device& D) {
   SV_HIP(hipMalloc(&D.btab, sv_btab_bytes()));
   SV_HIP(sv_launch_btab_init((uint32_t*)D.btab, D.stream));
   D.grid = (unsigned)(D.cus * sv_occupancy_blocks_per_cu());
+  D.grid_share = (unsigned)(D.cus * std::max(1, sv_share_blocks_per_cu()));
   SV_HIP(hipStreamSynchronize(D.stream));
   return SV_OK;
 }
@@ -400,16 +406,34 @@ int ensure_ws(Device& D, size_t bytes) {
   return D.ws.ensure(bytes);
 }
 
-unsigned grid_for(const Device& D, uint64_t n) {
+// Shared mode of the throughput kernels (sv_kernels.hip sv_launch_verify):
+// taken by every bulk launch within SV_LAT_SHARE_MS (default 1000) ms of a
+// latency-lane batch on the same slot, so SCP-class batches find free
+// workgroup slots while a tx set or catchup batch runs.  0 disables it.
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+int64_t share_window_ns() {
+  static const int64_t w = (int64_t)env_size("SV_LAT_SHARE_MS", 1000) * 1000000;
+  return w;
+}
+bool share_now(const Device& D) {
+  const int64_t w = share_window_ns();
+  return w > 0 && now_ns() - D.lat_last_ns.load(std::memory_order_relaxed) < w;
+}
+
+unsigned grid_for(const Device& D, uint64_t n, bool share = false) {
   const uint64_t need = (n + sv_block_threads() - 1) / sv_block_threads();
-  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(D.grid, need));
+  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(share ? D.grid_share : D.grid, need));
 }
 
 // Launch on D.stream (caller holds D.mu and has set the device).
 int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig, const void* msg, const uint64_t* off,
                   const uint32_t* len, uint32_t fixed_len, uint64_t n, void* verdict, void* bitmap) {
   const int rp = resolve_path(path, n);
-  const unsigned grid = grid_for(D, n);
+  const bool share = rp != SV_PATH_LATENCY && share_now(D);
+  const unsigned grid = grid_for(D, n, share);
   int rc;
   if ((rc = ensure_ws(D, sv_verify_ws_bytes(rp, grid, n)))) return rc;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -420,7 +444,8 @@ int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig
     SV_HIP(hipEventRecord(e0, D.stream));
   }
   SV_HIP(sv_launch_verify(mode, rp, grid, pk, sig, msg, off, len, fixed_len, n, verdict, bitmap, D.ws.p, D.btab,
-                          g_dbg.load() & kKernelDbgMask, D.stream));
+                          g_dbg.load() & kKernelDbgMask, share ? 1 : 0, D.stream));
+  if (share) D.shared_launches.fetch_add(1, std::memory_order_relaxed);
   if (timing) {
     SV_HIP(hipEventRecord(e1, D.stream));
     D.pending.emplace_back(e0, e1);
@@ -960,6 +985,7 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   int rc;
   if ((rc = lat_ready(D))) return rc;
   const auto t0 = std::chrono::steady_clock::now();
+  D.lat_last_ns.store(now_ns(), std::memory_order_relaxed);
   lat_cache_ready(L);
   lat_poll(L);
   const uint32_t dbg = g_dbg.load() & kKernelDbgMask;
@@ -1004,13 +1030,16 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
     const int mode = im.var ? 1 : (in.fixed == 32 ? 0 : 2);
     hipEvent_t e0;
     if ((rc = lat_timing_begin(L, &e0))) return rc;
+    // (while bulk work runs, only the 1-signature-per-wave geometry fits the
+    // slot a shared-mode bulk launch leaves free on each CU)
+    const bool bulk_busy = hipStreamQuery(D.stream) == hipErrorNotReady;
     if (warm)
-      SV_HIP(sv_launch_comb(mode, sv_comb_spw(n, D.cus), d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
+      SV_HIP(sv_launch_comb(mode, bulk_busy ? 1 : sv_comb_spw(n, D.cus), d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
                             d_verdict, (const uint32_t*)(d + o_ks), (const uint32_t*)L.ktab.p,
                             (const uint32_t*)L.kstat.p, (const uint32_t*)L.ctab, L.stream));
     else
       SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
-                              d_verdict, nullptr, nullptr, D.btab, dbg, L.stream));
+                              d_verdict, nullptr, nullptr, D.btab, dbg, 0, L.stream));
     if ((rc = lat_timing_end(L, e0, n))) return rc;
     t_k = std::chrono::steady_clock::now();
     if (!zc) SV_HIP(hipMemcpyAsync(ho, L.d_out.p, n, hipMemcpyDeviceToHost, L.stream));
@@ -1423,12 +1452,13 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
     std::lock_guard<std::mutex> g(L.mu);
     SV_HIP(hipSetDevice(D.phys));
     if ((rc = lat_ready(D))) return rc;
+    D.lat_last_ns.store(now_ns(), std::memory_order_relaxed);
     SV_HIP(hipEventRecord(L.ev_lat, user));
     SV_HIP(hipStreamWaitEvent(L.stream, L.ev_lat, 0));
     hipEvent_t e0;
     if ((rc = lat_timing_begin(L, &e0))) return rc;
     SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d_pk, d_sig, d_msg, d_msg_off, d_msg_len, fixed_msg_len, n,
-                            d_verdict, d_bitmap, nullptr, D.btab, g_dbg.load() & kKernelDbgMask, L.stream));
+                            d_verdict, d_bitmap, nullptr, D.btab, g_dbg.load() & kKernelDbgMask, 0, L.stream));
     if ((rc = lat_timing_end(L, e0, n))) return rc;
     SV_HIP(hipEventRecord(L.done, L.stream));
     SV_HIP(hipStreamWaitEvent(user, L.done, 0));
@@ -1596,6 +1626,7 @@ int sv_key_cache_get_stats(int device, sv_key_cache_stats* out) {
   out->cold_batches = L.cold;
   out->keys_built = L.built;
   out->evictions = L.evicted;
+  out->shared_launches = Dp->shared_launches.load();
   return SV_OK;
 }
 

@@ -121,6 +121,9 @@ __device__ __forceinline__ int32_t sv_sbyte(uint32_t w, uint32_t k) { return (in
 // One signature per SPW-th of a chain wave; see the file header.
 template <int MODE, int SPW>
 __global__ __launch_bounds__(256, 1) void sv_comb_kernel(sv_comb_params c) {
+  // Latency class: these waves win the SIMD's issue arbitration over a
+  // throughput kernel's waves sharing the CU (shared mode, sv_kernels.hip).
+  __builtin_amdgcn_s_setprio(3);
   constexpr int NS = SV_COMB_CHAIN_WAVES * SPW;  // signatures per workgroup
   constexpr int LPS = 64 / SPW;                  // lanes per signature
   constexpr int QPS = LPS / 4;                   // quads per signature

@@ -401,6 +401,7 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
 template <int MODE>
 __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams p) {
   __shared__ uint32_t s_tab[SV_OSIGS][2][SV_ATAB_ENTRIES][SV_QENT_DW];  // 23 KB
+  __builtin_amdgcn_s_setprio(3);  // latency class (as sv_comb_kernel)
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t role = lane & 3u, half = (lane >> 2) & 1u, sl = lane >> 3;
   const qd_role q{role == 1, role == 2, role == 3};
@@ -712,6 +713,18 @@ int sv_debug_phase_cycles(unsigned long long out[8], int reset) {
 }
 #endif
 
+#ifdef SV_MADCOUNT
+// (measurement builds: the field-product multiply-adds issued since the last reset)
+int sv_debug_madcount(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sv_madcount), sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned long long z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(sv_madcount), &z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
 size_t sv_ws_bytes_per_block(void) { return (size_t)SV_BLOCK * SV_SLOT_QUADS * sizeof(sv_u4); }
 
 // ------------------------------------------------- chunk planner (split path)
@@ -752,6 +765,29 @@ static int sv_wps(const void* kernel, std::atomic<int>& cache) {
 static std::atomic<int> g_main_wps{0}, g_prep_wps{0};
 static int sv_main_wps(void) { return sv_wps((const void*)sv_main_kernel, g_main_wps); }
 static int sv_prep_wps(void) { return sv_wps((const void*)sv_prep_kernel<0>, g_prep_wps); }
+// Shared mode (sv_launch_verify `share`): while latency-class batches are
+// live on the device, the throughput kernels leave one workgroup slot per CU
+// free for them -- the persistent main kernel runs one block per CU fewer
+// (the caller's grid) and each prep launch asks for enough dynamic LDS that
+// one block fewer fits per CU -- so a latency kernel (sv_comb_kernel<.,1>:
+// 146 VGPRs, 17 KB LDS; sv_octet_kernel: 166 VGPRs, 25 KB) is dispatched as
+// soon as it is queued instead of after a whole bulk chunk.
+static int sv_share_wps(int w) { return w > 1 ? w - 1 : 1; }
+static std::atomic<int> g_lds_cu{0};
+static size_t sv_prep_share_lds(void) {
+  int v = g_lds_cu.load(std::memory_order_relaxed);
+  if (v == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess || v < 1)
+      v = 160 * 1024;
+    g_lds_cu.store(v, std::memory_order_relaxed);
+  }
+  const int w = sv_share_wps(sv_prep_wps());  // blocks per CU wanted
+  size_t b = (size_t)v / (size_t)(w + 1) + 256;  // w + 1 blocks no longer fit
+  b = (b + 255) & ~(size_t)255;
+  return b > 65536 ? 65536 : b;
+}
 // SIMDs of the current device (4 per CU)
 static std::atomic<int> g_cus[64];
 static uint64_t sv_device_simds(void) {
@@ -770,11 +806,12 @@ static uint64_t sv_device_simds(void) {
 #ifndef SV_PLAN
 #define SV_PLAN 1  // 0: fixed SV_CHUNK-signature chunks (A/B baseline)
 #endif
-uint64_t sv_plan_chunk(uint64_t n) {
+uint64_t sv_plan_chunk(uint64_t n, int share) {
   if (!SV_PLAN) return SV_CHUNK;
   const uint64_t G = (n + 63) / 64;
   const uint64_t capG = SV_CHUNK / 64;
-  const int mw = sv_main_wps(), pw = sv_prep_wps();
+  const int mw = share ? sv_share_wps(sv_main_wps()) : sv_main_wps();
+  const int pw = share ? sv_share_wps(sv_prep_wps()) : sv_prep_wps();
   const uint64_t simds = sv_device_simds();
   if (G == 0 || simds == 0) return SV_CHUNK;
   const uint64_t kmin = (G + capG - 1) / capG;
@@ -804,7 +841,8 @@ uint64_t sv_plan_chunk(uint64_t n) {
 // chunk (sv_plan_chunk): the workspace of a batch of n holds ws_cap(n) of them,
 // rounded up to whole workgroups.
 uint64_t sv_ws_cap(uint64_t n) {
-  const uint64_t p = sv_plan_chunk(n);
+  const uint64_t p0 = sv_plan_chunk(n, 0), p1 = sv_plan_chunk(n, 1);
+  const uint64_t p = p0 > p1 ? p0 : p1;  // (either mode may run on one workspace)
   const uint64_t c = n < p ? n : p;
   return (c + SV_BLOCK - 1) / SV_BLOCK * SV_BLOCK;
 }
@@ -862,10 +900,15 @@ int sv_occupancy_blocks_per_cu(void) {
 #endif
 }
 
-// ws must hold sv_verify_ws_bytes(path, grid, n) bytes.
+// Blocks per CU of the persistent main kernel in shared mode.
+int sv_share_blocks_per_cu(void) { return sv_share_wps(sv_main_wps()) * 4 / (SV_BLOCK / 64); }
+
+// ws must hold sv_verify_ws_bytes(path, grid, n) bytes.  share: shared mode
+// (above); the caller's grid is then CUs x sv_share_blocks_per_cu().
 hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, const void* sig, const void* msg,
                             const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n,
-                            void* verdict, void* bitmap, void* ws, const void* btab, uint32_t dbg, hipStream_t s) {
+                            void* verdict, void* bitmap, void* ws, const void* btab, uint32_t dbg, int share,
+                            hipStream_t s) {
   sv_kparams p;
   p.pk = (const sv_u4*)pk;
   p.sig = (const sv_u4*)sig;
@@ -894,7 +937,8 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
   (void)path;
 #if SV_LATTICE && SV_SPLIT
   const uint64_t cap = sv_ws_cap(n);
-  const uint64_t chunk = sv_plan_chunk(n);
+  const uint64_t chunk = sv_plan_chunk(n, share);
+  const size_t plds = share ? sv_prep_share_lds() : 0;
   sv_u4* rec = p.ws + (size_t)cap * SV_SLOT_QUADS_L;
   uint32_t* wmax = (uint32_t*)(rec + (size_t)cap * SV_REC_QUADS);
   for (uint64_t start = 0; start < n; start += chunk) {
@@ -906,11 +950,11 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
     c.wmax = wmax;
     const unsigned pg = (unsigned)((c.cnt + SV_BLOCK - 1) / SV_BLOCK);
     if (mode == 0)
-      hipLaunchKernelGGL(sv_prep_kernel<0>, dim3(pg), dim3(SV_BLOCK), 0, s, c);
+      hipLaunchKernelGGL(sv_prep_kernel<0>, dim3(pg), dim3(SV_BLOCK), plds, s, c);
     else if (mode == 1)
-      hipLaunchKernelGGL(sv_prep_kernel<1>, dim3(pg), dim3(SV_BLOCK), 0, s, c);
+      hipLaunchKernelGGL(sv_prep_kernel<1>, dim3(pg), dim3(SV_BLOCK), plds, s, c);
     else
-      hipLaunchKernelGGL(sv_prep_kernel<2>, dim3(pg), dim3(SV_BLOCK), 0, s, c);
+      hipLaunchKernelGGL(sv_prep_kernel<2>, dim3(pg), dim3(SV_BLOCK), plds, s, c);
     if (!(dbg & SV_DBG_PREP_ONLY)) hipLaunchKernelGGL(sv_main_kernel, dim3(grid < pg ? grid : pg), dim3(SV_BLOCK), 0, s, c);
   }
 #else

@@ -307,3 +307,21 @@ def test_lattice_verdicts_independent_of_window_count(hostcore, golden):
         for wmin in (34, 41, 64):
             got, _ = _host_verify_lat(hostcore, d, rows, wmin)
             assert np.array_equal(got, d["verdict"][rows]), (name, wmin)
+
+
+def test_madcount_constants_match_generated_products():
+    """SV_MADS_MUL / SV_MADS_SQ (csrc/fe25519.h, the SV_MADCOUNT measurement
+    hook behind roofline.hw_mads_per_verify) equal the v_mad_u64_u32 count of
+    each generated product statement (csrc/fe_asm_gen.h)."""
+    import os
+    import re
+    csrc = os.path.join(REPO, "stellar-core_amd", "csrc")
+    gen = open(os.path.join(csrc, "fe_asm_gen.h")).read()
+    fe = open(os.path.join(csrc, "fe25519.h")).read()
+    const = {k: int(v) for k, v in re.findall(r"#define (SV_MADS_MUL|SV_MADS_SQ) (\d+)", fe)}
+    bodies = re.split(r"\nSV_HD void ", gen)[1:]
+    counts = {b.split("(")[0]: b.count("v_mad_u64_u32") for b in bodies}
+    assert counts, "no generated products found"
+    for name, c in counts.items():
+        want = const["SV_MADS_SQ"] if name.startswith("fe_sq") else const["SV_MADS_MUL"]
+        assert c == want, (name, c, want)

@@ -13,6 +13,6 @@ wait
 for o in variants/build/k_*.o; do
   name=${o#variants/build/k_}; name=${name%.o}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/libsv_$name.so $o \
-      stellar-core_amd/build/sv_api.o stellar-core_amd/build/sv_hash.o stellar-core_amd/build/sv_cpu.o -Wl,-rpath,/opt/rocm/lib -lpthread
+      stellar-core_amd/build/sv_api.o stellar-core_amd/build/sv_comb.o stellar-core_amd/build/sv_hash.o stellar-core_amd/build/sv_cpu.o -Wl,-rpath,/opt/rocm/lib -lpthread
 done
 ls -la variants/*.so
