@@ -161,6 +161,19 @@ class RandomEvictionCache {
     fcount_ = 0;  // the queued draws came from the old seed
   }
   void prefetch(Hash const& k) const { __builtin_prefetch(&table_[keyBits(k) & mask_]); }
+  // second stage of the walk's prefetch (the slot of k was prefetched a few
+  // items earlier): the entry of the first slot whose tag matches k
+  void prefetchFound(Hash const& k) const {
+    const uint64_t tag = keyBits(k) & 0xffffffffu;
+    for (size_t s = tag & mask_;; s = (s + 1) & mask_) {
+      const uint64_t t = table_[s];
+      if (t == 0) return;
+      if ((t >> 32) == tag) {
+        __builtin_prefetch(&entries_[(uint32_t)t - 1], 1);
+        return;
+      }
+    }
+  }
   uint32_t find(Hash const& k) const {
     const uint64_t tag = keyBits(k) & 0xffffffffu;
     for (size_t s = tag & mask_;; s = (s + 1) & mask_) {
@@ -284,6 +297,8 @@ class RandomEvictionCache {
         __builtin_prefetch(ordGen_.data() + b);
         __builtin_prefetch(ordTag_.data() + a);
         __builtin_prefetch(ordTag_.data() + b);
+        __builtin_prefetch(ordId_.data() + a);
+        __builtin_prefetch(ordId_.data() + b);
       }
     }
   }
@@ -294,10 +309,15 @@ class RandomEvictionCache {
     const size_t ia = future_[fhead_].first, ib = future_[fhead_].second;
     fhead_ = (fhead_ + 1) % kAhead;
     --fcount_;
-    {  // half-way ahead: the candidate victims' table slots
+    {  // half-way ahead: the candidate victims' table slots and entries (the
+       // victim's entry is rewritten by the next insert)
       auto const& f = future_[(fhead_ + kAhead / 2) % kAhead];
       __builtin_prefetch(&table_[ordTag_[f.first] & mask_]);
       __builtin_prefetch(&table_[ordTag_[f.second] & mask_]);
+      if (f.first < ordId_.size() && f.second < ordId_.size()) {
+        __builtin_prefetch(&entries_[ordId_[f.first]], 1);
+        __builtin_prefetch(&entries_[ordId_[f.second]], 1);
+      }
     }
     drawAhead();
     const size_t iv = ordGen_[ia] < ordGen_[ib] ? ia : ib;
@@ -535,6 +555,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
       owner = ++gBatchId;
       for (size_t e = 0; e < E; ++e) {
         if (e + 8 < E) gVerifySigCache.prefetch(keys[e + 8]);
+        if (e + 4 < E) gVerifySigCache.prefetchFound(keys[e + 4]);
         const uint32_t id = gVerifySigCache.find(keys[e]);
         if (id != kNone) {
           auto const& ent = gVerifySigCache.at(id);
@@ -607,6 +628,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
       owner = ++gBatchId;
       for (size_t e = 0; e < E; ++e) {
         if (e + 8 < E) gVerifySigCache.prefetch(keys[e + 8]);
+        if (e + 4 < E) gVerifySigCache.prefetchFound(keys[e + 4]);
         const uint32_t id = gVerifySigCache.find(keys[e]);
         if (id != RandomEvictionCache::kNone) {
           auto const& ent = gVerifySigCache.at(id);
