@@ -234,8 +234,26 @@ typedef struct sv_key_cache_stats {
                                mode because latency batches were live: they leave
                                one workgroup slot per CU to the latency lane
                                (window SV_LAT_SHARE_MS, default 1000; 0: off) */
+  uint64_t table_launches;  /* throughput-path launches that used the per-key tables */
+  uint64_t table_keys;      /* keys claimed in them since the tables were last cleared
+                               (as of the last launch whose counters came back) */
+  uint64_t table_clears;    /* times the claim words were cleared (claims reached half the slots) */
+  uint64_t table_slots;     /* slots of the per-key tables */
 } sv_key_cache_stats;
 int sv_key_cache_get_stats(int device, sv_key_cache_stats* out);
+
+/* Per-key tables of the throughput path (replaces, for repeated signers, the
+ * per-signature decode of A that libsodium's verify does,
+ * /root/reference/src/crypto/SecretKey.cpp:461-463 per call; catchup replays
+ * ~16 signatures per account, LedgerManagerImpl.cpp:1546-1609): each key's
+ * decoded -A and its 9-entry table are built once on the device and reused
+ * by every later signature of that key.  mode 0: off; 1: every throughput-
+ * path launch; 2 (default): host-buffer batches whose keys repeat (a sampled
+ * estimate; device-resident batches only with 1); -1: the SV_KEY_TABLES
+ * environment variable.  slots: table size (0: SV_KEY_TABLE_SLOTS or 2^19,
+ * ~1.5 KB of HBM each; claims stop at half, then the tables are cleared).
+ * Verdicts never depend on the tables.  Returns the previous mode. */
+int sv_set_key_tables(int mode, size_t slots);
 
 /* Test knobs (0 in production).  TRIVIAL_PAIR: every lane verifies through the
  * fallback pair (h, 1) of the half-size equation (lattice.h), i.e. the
@@ -250,6 +268,7 @@ int sv_key_cache_get_stats(int device, sv_key_cache_stats* out);
 #define SV_DBG_MAX_WINDOWS 0x2u
 #define SV_DBG_FAIL 0x4u
 #define SV_DBG_PREP_ONLY 0x8u
+#define SV_DBG_KEY_COLLIDE 0x10u /* every key gets the same per-key-table fingerprint (collision path) */
 int sv_set_debug_flags(uint32_t flags);
 
 /* Bytes of the slot's kernel workspace / pinned staging currently allocated. */

@@ -64,11 +64,11 @@ EXPORTED_SYMBOLS = (
     "sv_verify_cache_keys_device", "sv_sha256_device", "sv_set_kernel_path",
     "sv_ed25519_verify_batch_gather", "sv_ed25519_verify_batch_gather_cb", "sv_ed25519_verify_batch_cpu", "sv_ed25519_verify_cpu",
     "sv_set_device_map", "sv_set_min_shard", "sv_set_debug_flags", "sv_workspace_bytes", "sv_pinned_bytes",
-    "sv_set_key_cache", "sv_key_cache_wait", "sv_key_cache_get_stats",
+    "sv_set_key_cache", "sv_key_cache_wait", "sv_key_cache_get_stats", "sv_set_key_tables",
 )
 
 # test knobs (include/stellar_sigverify.h sv_set_debug_flags)
-DBG_TRIVIAL_PAIR, DBG_MAX_WINDOWS, DBG_FAIL, DBG_PREP_ONLY = 0x1, 0x2, 0x4, 0x8
+DBG_TRIVIAL_PAIR, DBG_MAX_WINDOWS, DBG_FAIL, DBG_PREP_ONLY, DBG_KEY_COLLIDE = 0x1, 0x2, 0x4, 0x8, 0x10
 
 
 class SigVerifyError(RuntimeError):
@@ -82,7 +82,8 @@ class sv_opts(ctypes.Structure):
 
 class KeyCacheStats(ctypes.Structure):
     _fields_ = [(f, ctypes.c_uint64) for f in ("capacity", "keys", "warm_batches", "cold_batches", "keys_built",
-                                                "evictions", "shared_launches")]
+                                                "evictions", "shared_launches", "table_launches", "table_keys",
+                                                "table_clears", "table_slots")]
 
 
 _lib: Optional[ctypes.CDLL] = None
@@ -137,6 +138,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sv_workspace_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
     lib.sv_pinned_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
     lib.sv_set_key_cache.argtypes = [sz]
+    lib.sv_set_key_tables.argtypes = [ctypes.c_int, sz]
     lib.sv_key_cache_wait.argtypes = [ctypes.c_int]
     lib.sv_key_cache_get_stats.argtypes = [ctypes.c_int, ctypes.POINTER(KeyCacheStats)]
     _lib = lib
@@ -393,6 +395,16 @@ def synchronize(device: int = 0) -> None:
 def set_key_cache(capacity: int) -> None:
     """Key-cache capacity of the warm-key latency path (0: off); clears it."""
     _check(load_library().sv_set_key_cache(int(capacity)))
+
+
+def set_key_tables(mode: int, slots: int = 0) -> int:
+    """Per-key tables of the throughput path: 0 off, 1 on, 2 auto (host
+    batches whose keys repeat), -1 the SV_KEY_TABLES default; slots 0 keeps
+    SV_KEY_TABLE_SLOTS / 2^19.  Returns the previous mode."""
+    rc = load_library().sv_set_key_tables(int(mode), int(slots))
+    if rc < -1:
+        _check(rc)
+    return rc
 
 
 def key_cache_wait(device: int = 0) -> None:

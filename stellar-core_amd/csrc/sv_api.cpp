@@ -41,6 +41,7 @@
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <random>
 #include <string>
 #include <thread>
 #include <vector>
@@ -48,6 +49,7 @@
 #include "../../include/stellar_sigverify.h"
 #include "comb.h"
 #include "keycache.h"
+#include "keytab.h"
 #include "pool.h"
 
 extern "C" {
@@ -60,8 +62,10 @@ int sv_occupancy_blocks_per_cu(void);
 hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, const void* sig, const void* msg,
                             const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n,
                             void* verdict, void* bitmap, void* ws, const void* btab, uint32_t dbg, int share,
-                            hipStream_t s);
+                            const sv_ktparams* kt, hipStream_t s);
 int sv_share_blocks_per_cu(void);
+size_t sv_key_table_entry_bytes(void);
+uint64_t sv_plan_chunk_max(uint64_t n);
 hipError_t sv_launch_sign(unsigned grid, const void* seed, const void* msg, uint64_t n, void* pk, void* sig,
                           void* ws, const void* btab, hipStream_t s);
 hipError_t sv_launch_hash(int kind, unsigned max_blocks, const void* pk, const void* sig, const void* msg,
@@ -213,6 +217,19 @@ struct LatLane {
   uint64_t warm = 0, cold = 0, built = 0, evicted = 0;
 };
 
+// Per-key tables of the throughput path (sv_kernels.hip sv_keyslot_kernel),
+// one set per slot: claim words, entries, per-chunk slot and builder lists,
+// the two counters and a pinned copy of them (read lazily: the claims decide
+// when the claim words are cleared, never a verdict).
+struct KeyTabs {
+  DevBuf index, store, kslot, builders, count;
+  HostBuf h_count;
+  hipEvent_t copied = nullptr;  // h_count holds the counters after the last launch
+  size_t slots = 0;
+  uint64_t salt = 0;
+  uint64_t launches = 0, clears = 0, claims = 0;
+};
+
 struct Device {
   int slot = -1;
   int phys = -1;
@@ -234,6 +251,7 @@ struct Device {
   double total_ms = 0;
   uint64_t launches = 0, sigs = 0;
   LatLane lat;
+  KeyTabs kt;  // (under mu)
   std::atomic<int64_t> lat_last_ns{INT64_MIN / 2};  // steady clock of the last latency-lane batch
   std::atomic<uint64_t> shared_launches{0};          // bulk launches in shared mode
 };
@@ -248,7 +266,7 @@ std::atomic<uint32_t> g_dbg{0};          // sv_set_debug_flags
 std::atomic<size_t> g_min_shard{0};      // sv_set_min_shard (0: default)
 std::atomic<uint64_t> g_rr{0};           // round-robin slot for single-slot calls
 
-constexpr uint32_t kKernelDbgMask = SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_PREP_ONLY;
+constexpr uint32_t kKernelDbgMask = SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_PREP_ONLY | SV_DBG_KEY_COLLIDE;
 
 // Batches up to this size take the latency kernel under SV_PATH_AUTO
 // (measured crossover on MI355X).
@@ -336,6 +354,11 @@ void release_device(Device& D) {
   }
   D.msg.release(); D.off.release(); D.len.release(); D.keys.release(); D.h_sha.release();
   D.ws.release();
+  D.kt.index.release(); D.kt.store.release(); D.kt.kslot.release(); D.kt.builders.release();
+  D.kt.count.release(); D.kt.h_count.release();
+  if (D.kt.copied) (void)hipEventDestroy(D.kt.copied);
+  D.kt.copied = nullptr;
+  D.kt.slots = 0;
   if (D.btab) (void)hipFree(D.btab);
   if (D.dep_in) (void)hipEventDestroy(D.dep_in);
   if (D.dep_out) (void)hipEventDestroy(D.dep_out);
@@ -428,14 +451,89 @@ unsigned grid_for(const Device& D, uint64_t n, bool share = false) {
   return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(share ? D.grid_share : D.grid, need));
 }
 
-// Launch on D.stream (caller holds D.mu and has set the device).
+// ---------------------------------------------------- per-key tables
+// sv_set_key_tables: 0 off, 1 on for every throughput-path launch, 2 (auto,
+// the default) on for host-buffer batches whose keys repeat (repeated_keys);
+// -1: SV_KEY_TABLES.  Slots: SV_KEY_TABLE_SLOTS (default 2^19; claims stop at
+// half of them, when the claim words are cleared).
+std::atomic<int> g_kt_mode{-1};
+std::atomic<size_t> g_kt_slots{0};
+int kt_mode() {
+  const int v = g_kt_mode.load();
+  if (v >= 0) return v;
+  return (int)std::min<size_t>(2, env_size("SV_KEY_TABLES", 2));
+}
+size_t kt_slots() {
+  size_t v = g_kt_slots.load();
+  if (v == 0) v = env_size("SV_KEY_TABLE_SLOTS", (size_t)1 << 19);
+  size_t p = 1024;
+  while (p < v && p < ((size_t)1 << 26)) p <<= 1;
+  return p;
+}
+
+// Readies the slot's key tables for a launch of n (caller holds D.mu, device
+// set) and fills *kt; false: tables unavailable (allocation failed), the
+// launch runs without them.
+bool kt_prepare(Device& D, uint64_t n, sv_ktparams* kt) {
+  KeyTabs& T = D.kt;
+  const size_t want = kt_slots();
+  if (T.slots != want) {
+    (void)hipStreamSynchronize(D.stream);
+    T.index.release();
+    T.store.release();
+    T.slots = 0;
+    if (T.index.ensure(want * 8) || T.store.ensure(want * sv_key_table_entry_bytes()) || T.count.ensure(16) ||
+        T.h_count.ensure(16))
+      return false;
+    if (!T.copied && hipEventCreateWithFlags(&T.copied, hipEventDisableTiming) != hipSuccess) return false;
+    if (hipMemsetAsync(T.index.p, 0, want * 8, D.stream) != hipSuccess ||
+        hipMemsetAsync(T.count.p, 0, 16, D.stream) != hipSuccess)
+      return false;
+    std::memset(T.h_count.p, 0, 16);
+    T.salt = ((uint64_t)std::random_device{}() << 32) ^ std::random_device{}() ^ (uint64_t)now_ns();
+    T.slots = want;
+  }
+  const uint64_t cap = sv_plan_chunk_max(n);
+  if (cap * 4 > T.kslot.cap || cap * 4 > T.builders.cap) {
+    (void)hipStreamSynchronize(D.stream);  // (the lists of a running launch)
+    if (T.kslot.ensure(cap * 4) || T.builders.ensure(cap * 4)) return false;
+  }
+  // the claims as of the last launch whose counters have come back
+  const uint32_t limit = (uint32_t)(want / 2);
+  if (hipEventQuery(T.copied) == hipSuccess) {
+    T.claims = ((const uint32_t*)T.h_count.p)[1];
+    if (T.claims >= limit) {
+      if (hipMemsetAsync(T.index.p, 0, want * 8, D.stream) != hipSuccess ||
+          hipMemsetAsync(T.count.p, 0, 16, D.stream) != hipSuccess)
+        return false;
+      std::memset(T.h_count.p, 0, 16);
+      T.claims = 0;
+      ++T.clears;
+    }
+  }
+  kt->index = (unsigned long long*)T.index.p;
+  kt->store = (sv_u4*)T.store.p;
+  kt->kslot = (uint32_t*)T.kslot.p;
+  kt->builders = (uint32_t*)T.builders.p;
+  kt->count = (uint32_t*)T.count.p;
+  kt->mask = want - 1;
+  kt->limit = limit;
+  kt->salt = T.salt;
+  return true;
+}
+
+// Launch on D.stream (caller holds D.mu and has set the device).  tables:
+// the launch may use the per-key tables (kt_mode / repeated_keys).
 int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig, const void* msg, const uint64_t* off,
-                  const uint32_t* len, uint32_t fixed_len, uint64_t n, void* verdict, void* bitmap) {
+                  const uint32_t* len, uint32_t fixed_len, uint64_t n, void* verdict, void* bitmap,
+                  bool tables = false) {
   const int rp = resolve_path(path, n);
   const bool share = rp != SV_PATH_LATENCY && share_now(D);
   const unsigned grid = grid_for(D, n, share);
   int rc;
   if ((rc = ensure_ws(D, sv_verify_ws_bytes(rp, grid, n)))) return rc;
+  sv_ktparams ktp{};
+  const bool kt_on = tables && rp != SV_PATH_LATENCY && kt_prepare(D, n, &ktp);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool timing = g_timing.load() != 0;
   if (timing) {
@@ -444,8 +542,13 @@ int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig
     SV_HIP(hipEventRecord(e0, D.stream));
   }
   SV_HIP(sv_launch_verify(mode, rp, grid, pk, sig, msg, off, len, fixed_len, n, verdict, bitmap, D.ws.p, D.btab,
-                          g_dbg.load() & kKernelDbgMask, share ? 1 : 0, D.stream));
+                          g_dbg.load() & kKernelDbgMask, share ? 1 : 0, kt_on ? &ktp : nullptr, D.stream));
   if (share) D.shared_launches.fetch_add(1, std::memory_order_relaxed);
+  if (kt_on) {
+    ++D.kt.launches;
+    SV_HIP(hipMemcpyAsync(D.kt.h_count.p, D.kt.count.p, 8, hipMemcpyDeviceToHost, D.stream));
+    SV_HIP(hipEventRecord(D.kt.copied, D.stream));
+  }
   if (timing) {
     SV_HIP(hipEventRecord(e1, D.stream));
     D.pending.emplace_back(e0, e1);
@@ -599,6 +702,35 @@ int drain_stage(Stage& s, uint8_t* verdict, uint8_t* keys) {
 
 typedef void (*KeysReadyFn)(void*);
 
+// Do the keys of a host batch repeat?  A sample of up to 4096 evenly spaced
+// rows: with s sampled of n and d repeats among them, K distinct keys give
+// d ~ s^2 / 2K, so K <= n / 2 (each key signs twice on average) reads as
+// d * n >= s^2 (exact when s = n: n - d <= n / 2).
+bool repeated_keys(const HostIn& in, size_t n) {
+  const size_t s = std::min<size_t>(n, 4096);
+  if (s < 2) return false;
+  constexpr size_t kSet = 8192;
+  std::vector<const uint8_t*> set(kSet, nullptr);
+  size_t d = 0;
+  for (size_t k = 0; k < s; ++k) {
+    const uint8_t* pk = in.pkp(k * n / s);
+    uint64_t h;
+    std::memcpy(&h, pk, 8);
+    h *= 0x9E3779B97F4A7C15ull;
+    for (size_t j = (size_t)(h >> 51) & (kSet - 1);; j = (j + 1) & (kSet - 1)) {
+      if (!set[j]) {
+        set[j] = pk;
+        break;
+      }
+      if (std::memcmp(set[j], pk, 32) == 0) {
+        ++d;
+        break;
+      }
+    }
+  }
+  return s == n ? 2 * (n - d) <= n : (uint64_t)d * n >= (uint64_t)s * s;
+}
+
 // Host-buffer slice on one slot, pipelined over staging chunks: verdicts
 // (verdict != null) and/or BLAKE2b cache keys (keys != null) into the
 // caller's arrays.  keys_cb (optional, with keys and verdict): called once
@@ -609,6 +741,9 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
                       KeysReadyFn keys_cb, void* cb_ctx, bool* cb_done) {
   const size_t chunk = std::min(n, stage_chunk());
   int rc;
+  const int ktm = kt_mode();
+  const bool tables = verdict && resolve_path(path, chunk) != SV_PATH_LATENCY &&
+                      (ktm == 1 || (ktm == 2 && repeated_keys(in, n)));
   // the largest launch first, so the workspace never grows under a running kernel
   if (verdict && (rc = ensure_ws(D, sv_verify_ws_bytes(resolve_path(path, chunk), grid_for(D, chunk), chunk))))
     return rc;
@@ -665,7 +800,7 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     if (verdict) {
       const int mode = im.var ? 1 : (in.fixed == 32 ? 0 : 2);
       if ((rc = launch_locked(D, mode, path, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m,
-                              s.d_verdict.p, nullptr)))
+                              s.d_verdict.p, nullptr, tables)))
         return rc;
     }
     if (!single) {
@@ -1039,7 +1174,7 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
                             (const uint32_t*)L.kstat.p, (const uint32_t*)L.ctab, L.stream));
     else
       SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
-                              d_verdict, nullptr, nullptr, D.btab, dbg, 0, L.stream));
+                              d_verdict, nullptr, nullptr, D.btab, dbg, 0, nullptr, L.stream));
     if ((rc = lat_timing_end(L, e0, n))) return rc;
     t_k = std::chrono::steady_clock::now();
     if (!zc) SV_HIP(hipMemcpyAsync(ho, L.d_out.p, n, hipMemcpyDeviceToHost, L.stream));
@@ -1458,7 +1593,7 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
     hipEvent_t e0;
     if ((rc = lat_timing_begin(L, &e0))) return rc;
     SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d_pk, d_sig, d_msg, d_msg_off, d_msg_len, fixed_msg_len, n,
-                            d_verdict, d_bitmap, nullptr, D.btab, g_dbg.load() & kKernelDbgMask, 0, L.stream));
+                            d_verdict, d_bitmap, nullptr, D.btab, g_dbg.load() & kKernelDbgMask, 0, nullptr, L.stream));
     if ((rc = lat_timing_end(L, e0, n))) return rc;
     SV_HIP(hipEventRecord(L.done, L.stream));
     SV_HIP(hipStreamWaitEvent(user, L.done, 0));
@@ -1469,8 +1604,9 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
   if ((rc = ready_locked(D))) return rc;
   SV_HIP(hipEventRecord(D.dep_in, user));
   SV_HIP(hipStreamWaitEvent(D.stream, D.dep_in, 0));
+  // (auto mode cannot look at device-resident keys: tables only when on)
   if ((rc = launch_locked(D, mode, SV_PATH_AUTO, d_pk, d_sig, d_msg, d_msg_off, d_msg_len, fixed_msg_len, n,
-                          d_verdict, d_bitmap)))
+                          d_verdict, d_bitmap, kt_mode() == 1)))
     return rc;
   SV_HIP(hipEventRecord(D.dep_out, D.stream));
   SV_HIP(hipStreamWaitEvent(user, D.dep_out, 0));
@@ -1483,7 +1619,8 @@ int sv_set_kernel_path(int path) {
 }
 
 int sv_set_debug_flags(uint32_t flags) {
-  if (flags & ~(SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_FAIL | SV_DBG_PREP_ONLY)) return SV_ERR_INVALID_ARG;
+  if (flags & ~(SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_FAIL | SV_DBG_PREP_ONLY | SV_DBG_KEY_COLLIDE))
+    return SV_ERR_INVALID_ARG;
   // the knobs that change what a call returns (FAIL: every call errs;
   // PREP_ONLY: no verdicts) only exist for processes that opt in
   if ((flags & (SV_DBG_FAIL | SV_DBG_PREP_ONLY)) && !test_knobs_enabled())
@@ -1582,6 +1719,12 @@ int sv_device_synchronize(int device) {
   return SV_OK;
 }
 
+int sv_set_key_tables(int mode, size_t slots) {
+  if (mode < -1 || mode > 2) return fail(SV_ERR_INVALID_ARG, "key-table mode must be -1, 0, 1 or 2");
+  g_kt_slots.store(slots);
+  return g_kt_mode.exchange(mode);
+}
+
 int sv_set_key_cache(size_t capacity) {
   if (capacity > ((size_t)1 << 20)) return fail(SV_ERR_INVALID_ARG, "key cache capacity above 2^20 keys");
   std::lock_guard<std::mutex> g0(g_mu);
@@ -1627,6 +1770,15 @@ int sv_key_cache_get_stats(int device, sv_key_cache_stats* out) {
   out->keys_built = L.built;
   out->evictions = L.evicted;
   out->shared_launches = Dp->shared_launches.load();
+  {
+    std::lock_guard<std::mutex> g2(Dp->mu);
+    KeyTabs& T = Dp->kt;
+    if (T.slots && T.copied && hipEventQuery(T.copied) == hipSuccess) T.claims = ((const uint32_t*)T.h_count.p)[1];
+    out->table_launches = T.launches;
+    out->table_keys = T.claims;
+    out->table_clears = T.clears;
+    out->table_slots = T.slots ? T.slots : kt_slots();
+  }
   return SV_OK;
 }
 

@@ -19,6 +19,7 @@
 #include "verify_core.h"
 #include "quad.h"
 #include "sv_kparams.h"
+#include "keytab.h"
 
 #define SV_BLOCK 256
 #ifndef SV_STAGE_A
@@ -43,6 +44,7 @@
 #define SV_DBG_TRIVIAL_PAIR 1u  // every lane takes the fallback pair (h, 1)
 #define SV_DBG_MAX_WINDOWS 2u   // every wave runs 64 windows
 #define SV_DBG_PREP_ONLY 8u     // split path: prep kernel only (profiling; no verdicts)
+#define SV_DBG_KEY_COLLIDE 16u  // per-key tables: every key gets the same fingerprint (collision path)
 __device__ __forceinline__ int sv_wave_windows(int wl, uint32_t dbg) {
   int W = (dbg & SV_DBG_MAX_WINDOWS) ? 64 : SV_LAT_MIN_WINDOWS;
   while (__ballot(wl > W) != 0) ++W;
@@ -93,12 +95,30 @@ __device__ unsigned long long sv_phase_cycles[8];
 #endif
 #define SV_REC_QUADS ((16 + 2 * SV_LB_DIGITS + 1 + 3) / 4)
 // record: dA[8] dR[8] dB0[SV_LB_DIGITS] dB1[SV_LB_DIGITS] flags (9 quads at radix 2^16)
-static_assert(16 + 2 * SV_LB_DIGITS + 1 <= 4 * SV_REC_QUADS, "digit record size");
+static_assert(16 + 2 * SV_LB_DIGITS + 2 <= 4 * SV_REC_QUADS, "digit record size");
 // record flags
 #define SV_REC_RNEG 1u
 #define SV_REC_TOP8A 2u
 #define SV_REC_TOP8R 4u
 #define SV_REC_OK 8u
+
+// ------------------------------------- per-key tables (throughput path)
+// Catchup checkpoints, tx sets and SCP traffic sign with far fewer keys than
+// signatures (a checkpoint: ~16 signatures per account).  With per-key tables
+// on, each chunk first maps every signature's key to a slot of a persistent
+// device table (sv_keyslot_kernel: one claim word per slot, compare-and-swap
+// on a salted 64-bit fingerprint of the key); the first signature to claim a
+// slot queues it, and sv_keybuild_kernel decodes each queued key ONCE
+// (compacted: one lane per new key) into its entry: the key's 9 cached
+// multiples of -A and a status bit (A canonical, not small-order, decodes).
+// The prep kernel then skips A's square root and table build for a wave
+// whose 64 keys all have a built entry with exactly their 32 bytes (a
+// fingerprint collision or a full probe run leaves the lane's key uncached:
+// the wave decodes inline as without tables), and the main kernel reads
+// table_A from the entry.  Decoding is deterministic, so verdicts do not
+// depend on the tables.  Entries are never modified after their build; the
+// host clears the claim words when the claims reach `limit` (sv_api.cpp).
+static_assert(SV_KT_TQUADS == SV_ATAB_ENTRIES * SV_LTAB_QUADS, "key-table entry layout");
 
 struct sv_cparams {
   sv_kparams k;
@@ -106,9 +126,74 @@ struct sv_cparams {
   uint64_t cnt;    // signatures in the chunk (<= SV_CHUNK)
   sv_u4* rec;      // SV_CHUNK x SV_REC_QUADS
   uint32_t* wmax;  // SV_CHUNK / 64
+  sv_ktparams kt;
 };
 
-template <int MODE>
+__device__ __forceinline__ unsigned long long sv_kt_fp(const uint32_t A[8], uint64_t salt, uint32_t dbg) {
+  if (dbg & SV_DBG_KEY_COLLIDE) return 1ull;
+  uint64_t h = salt;
+  SV_UNROLL for (int i = 0; i < 8; ++i) {
+    h = (h ^ A[i]) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+  }
+  return h | 1ull;
+}
+
+// Slot of every signature's key (one lane per signature of the chunk).
+__global__ __launch_bounds__(SV_BLOCK) void sv_keyslot_kernel(sv_cparams c) {
+  const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= c.cnt) return;
+  const sv_ktparams& t = c.kt;
+  uint32_t A[8];
+  sv_unpack2(A, c.k.pk + 2 * (c.start + li));
+  const unsigned long long fp = sv_kt_fp(A, t.salt, c.k.dbg);
+  uint32_t ks = SV_KT_NONE;
+  for (int q = 0; q < SV_KT_PROBES; ++q) {
+    const uint64_t s = ((fp >> 17) + (uint64_t)q) & t.mask;
+    unsigned long long w = __hip_atomic_load(&t.index[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w == 0ull) {
+      if (__hip_atomic_load(&t.count[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= t.limit) break;
+      w = atomicCAS(&t.index[s], 0ull, fp);
+      if (w == 0ull) {  // claimed: sv_keybuild_kernel decodes this key into slot s
+        sv_u4* e = t.store + s * SV_KT_QUADS + SV_KT_TQUADS;
+        e[0] = sv_u4{A[0], A[1], A[2], A[3]};
+        e[1] = sv_u4{A[4], A[5], A[6], A[7]};
+        t.builders[atomicAdd(&t.count[0], 1u)] = (uint32_t)s;
+        atomicAdd(&t.count[1], 1u);
+        ks = (uint32_t)s;
+        break;
+      }
+    }
+    if (w == fp) {  // (the prep kernel compares the entry's 32 bytes)
+      ks = (uint32_t)s;
+      break;
+    }
+  }
+  t.kslot[li] = ks;
+}
+
+// Decodes the keys claimed in this chunk, one lane per key.
+__global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_keybuild_kernel(sv_cparams c) {
+  const sv_ktparams& t = c.kt;
+  const uint32_t nb = t.count[0];
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  if (i - lane >= nb) return;  // (wave-uniform)
+  const bool active = i < nb;
+  const uint32_t s = t.builders[active ? i : nb - 1];  // (idle tail lanes redo the last key: same bytes)
+  sv_u4* e = t.store + (uint64_t)s * SV_KT_QUADS;
+  uint32_t A[8];
+  sv_unpack2(A, e + SV_KT_TQUADS);
+  bool ok = sv_point_canonical(A) && !sv_small_order(A);
+  ge_p3 negA;
+  ok = ge_frombytes(negA, A, true) && ok;
+  sv_build_ltab(e, negA);
+  if (active) e[SV_KT_TQUADS + 2] = sv_u4{ok ? 1u : 0u, 0u, 0u, 0u};
+}
+
+// KT: per-key tables on (a separate instantiation, so the tables-off path
+// carries none of their code)
+template <int MODE, bool KT>
 __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cparams c) {
   const sv_kparams& p = c.k;
   const uint32_t lane = threadIdx.x & 63u;
@@ -138,6 +223,23 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   sv_unpack2(R, p.sig + 4 * ii);
 #endif
   SV_PHASE(0);
+  // per-key tables: skip A for a wave whose keys all have a built entry
+  int a_status = -1;
+  uint32_t ks = SV_KT_NONE;
+  if (KT) {
+    ks = c.kt.kslot[active ? li : c.cnt - 1];
+    bool hit = false;
+    uint32_t st = 0;
+    if (ks != SV_KT_NONE) {
+      const sv_u4* e = c.kt.store + (uint64_t)ks * SV_KT_QUADS + SV_KT_TQUADS;
+      const sv_u4 k0 = e[0], k1 = e[1], k2 = e[2];
+      hit = k0.x == A[0] && k0.y == A[1] && k0.z == A[2] && k0.w == A[3] && k1.x == A[4] && k1.y == A[5] &&
+            k1.z == A[6] && k1.w == A[7];
+      st = k2.x;
+    }
+    if (__ballot(!hit) == 0) a_status = (int)(st & 1u);
+    else ks = SV_KT_NONE;
+  }
   sv_lat lat;
 #ifdef SV_PHASE_PROF
   bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
@@ -156,7 +258,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   sv_build_ltab(tabR, negR);
   SV_PHASE(3);
 #else
-  const bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
+  const bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0, a_status);
 #endif
   const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
   sv_lat_digits D;
@@ -174,6 +276,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
     rw[16 + SV_LB_DIGITS + k] = (uint32_t)D.dB1[k];
   }
   rw[16 + 2 * SV_LB_DIGITS] = flags;
+  rw[16 + 2 * SV_LB_DIGITS + 1] = ks;  // table_A: key entry ks, or (SV_KT_NONE) the lane's slot
   sv_u4* r = c.rec + li * SV_REC_QUADS;
   SV_UNROLL for (int k = 0; k < SV_REC_QUADS; ++k) r[k] = sv_u4{rw[4 * k], rw[4 * k + 1], rw[4 * k + 2], rw[4 * k + 3]};
   if (lane == 0) c.wmax[li >> 6] = (uint32_t)W;
@@ -304,6 +407,7 @@ __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw,
 #endif
 }
 
+template <bool KT>
 __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cparams c) {
   const sv_kparams& p = c.k;
   __shared__ sv_u4 s_stage[SV_BLOCK / 64][(SV_STAGE_ONE ? 1 : 2) * SV_LTAB_QUADS * 64];  // per-wave entry stage
@@ -316,10 +420,15 @@ __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cpa
   for (uint64_t base = gtid - lane; base < c.cnt; base += stride) {
     const uint64_t li = base + lane;  // (slots exist up to the chunk's last full wave)
     const bool active = li < c.cnt;
-    const sv_u4* tabA = p.ws + li * SV_SLOT_QUADS_L;
-    const sv_u4* tabR = tabA + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
+    const sv_u4* slot = p.ws + li * SV_SLOT_QUADS_L;
+    const sv_u4* tabR = slot + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
     const uint32_t* rw = (const uint32_t*)(c.rec + li * SV_REC_QUADS);
     const uint32_t flags = rw[16 + 2 * SV_LB_DIGITS];
+    const sv_u4* tabA = slot;
+    if (KT) {
+      const uint32_t ks = rw[16 + 2 * SV_LB_DIGITS + 1];
+      if (ks != SV_KT_NONE) tabA = c.kt.store + (uint64_t)ks * SV_KT_QUADS;
+    }
     const bool pre_ok = (flags & SV_REC_OK) != 0;
     const int W = (int)__builtin_amdgcn_readfirstlane(c.wmax[li >> 6]);
     ge_p3 P;
@@ -763,8 +872,8 @@ static int sv_wps(const void* kernel, std::atomic<int>& cache) {
   return w;
 }
 static std::atomic<int> g_main_wps{0}, g_prep_wps{0};
-static int sv_main_wps(void) { return sv_wps((const void*)sv_main_kernel, g_main_wps); }
-static int sv_prep_wps(void) { return sv_wps((const void*)sv_prep_kernel<0>, g_prep_wps); }
+static int sv_main_wps(void) { return sv_wps((const void*)sv_main_kernel<false>, g_main_wps); }
+static int sv_prep_wps(void) { return sv_wps((const void*)sv_prep_kernel<0, false>, g_prep_wps); }
 // Shared mode (sv_launch_verify `share`): while latency-class batches are
 // live on the device, the throughput kernels leave one workgroup slot per CU
 // free for them -- the persistent main kernel runs one block per CU fewer
@@ -889,7 +998,7 @@ hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s) {
 int sv_occupancy_blocks_per_cu(void) {
   int b0 = 0, b1 = 0, b2 = 0, b3 = 0;
 #if SV_LATTICE && SV_SPLIT
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, sv_main_kernel, SV_BLOCK, 0) != hipSuccess) b0 = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, sv_main_kernel<false>, SV_BLOCK, 0) != hipSuccess) b0 = 1;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b3, sv_sign_kernel, SV_BLOCK, 0) != hipSuccess) b3 = 1;
   const int ms = b0 > b3 ? b0 : b3;
   (void)b1;
@@ -900,15 +1009,20 @@ int sv_occupancy_blocks_per_cu(void) {
 #endif
 }
 
+size_t sv_key_table_entry_bytes(void) { return (size_t)SV_KT_QUADS * sizeof(sv_u4); }
+uint64_t sv_plan_chunk_max(uint64_t n) { return sv_ws_cap(n); }
+
 // Blocks per CU of the persistent main kernel in shared mode.
 int sv_share_blocks_per_cu(void) { return sv_share_wps(sv_main_wps()) * 4 / (SV_BLOCK / 64); }
 
 // ws must hold sv_verify_ws_bytes(path, grid, n) bytes.  share: shared mode
-// (above); the caller's grid is then CUs x sv_share_blocks_per_cu().
+// (above); the caller's grid is then CUs x sv_share_blocks_per_cu().  kt
+// (optional): per-key tables (above); kt->kslot / kt->builders hold
+// sv_plan_chunk(n) entries, kt->count 2.
 hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, const void* sig, const void* msg,
                             const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n,
                             void* verdict, void* bitmap, void* ws, const void* btab, uint32_t dbg, int share,
-                            hipStream_t s) {
+                            const sv_ktparams* kt, hipStream_t s) {
   sv_kparams p;
   p.pk = (const sv_u4*)pk;
   p.sig = (const sv_u4*)sig;
@@ -948,14 +1062,30 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
     c.cnt = n - start < chunk ? n - start : chunk;
     c.rec = rec;
     c.wmax = wmax;
+    c.kt = kt ? *kt : sv_ktparams{};
     const unsigned pg = (unsigned)((c.cnt + SV_BLOCK - 1) / SV_BLOCK);
-    if (mode == 0)
-      hipLaunchKernelGGL(sv_prep_kernel<0>, dim3(pg), dim3(SV_BLOCK), plds, s, c);
-    else if (mode == 1)
-      hipLaunchKernelGGL(sv_prep_kernel<1>, dim3(pg), dim3(SV_BLOCK), plds, s, c);
-    else
-      hipLaunchKernelGGL(sv_prep_kernel<2>, dim3(pg), dim3(SV_BLOCK), plds, s, c);
-    if (!(dbg & SV_DBG_PREP_ONLY)) hipLaunchKernelGGL(sv_main_kernel, dim3(grid < pg ? grid : pg), dim3(SV_BLOCK), 0, s, c);
+    if (kt) {
+      const hipError_t e = hipMemsetAsync(kt->count, 0, sizeof(uint32_t), s);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(sv_keyslot_kernel, dim3(pg), dim3(SV_BLOCK), 0, s, c);
+      hipLaunchKernelGGL(sv_keybuild_kernel, dim3(pg), dim3(SV_BLOCK), 0, s, c);
+    }
+#define SV_PREP_LAUNCH(M, K) hipLaunchKernelGGL((sv_prep_kernel<M, K>), dim3(pg), dim3(SV_BLOCK), plds, s, c)
+    if (kt) {
+      if (mode == 0) SV_PREP_LAUNCH(0, true);
+      else if (mode == 1) SV_PREP_LAUNCH(1, true);
+      else SV_PREP_LAUNCH(2, true);
+    } else {
+      if (mode == 0) SV_PREP_LAUNCH(0, false);
+      else if (mode == 1) SV_PREP_LAUNCH(1, false);
+      else SV_PREP_LAUNCH(2, false);
+    }
+#undef SV_PREP_LAUNCH
+    if (!(dbg & SV_DBG_PREP_ONLY)) {
+      const dim3 mg(grid < pg ? grid : pg);
+      if (kt) hipLaunchKernelGGL(sv_main_kernel<true>, mg, dim3(SV_BLOCK), 0, s, c);
+      else hipLaunchKernelGGL(sv_main_kernel<false>, mg, dim3(SV_BLOCK), 0, s, c);
+    }
   }
 #else
 #error "the product build is the split half-size path (SV_LATTICE = SV_SPLIT = 1)"

@@ -780,10 +780,22 @@ SV_HD bool sv_is_identity(const ge_p3& P) {
 #ifndef SV_PREP_SEQ
 #define SV_PREP_SEQ 1
 #endif
+// a_status >= 0 (SV_PREP_SEQ 1): A's checks and decode are already known --
+// a_status != 0 iff A is canonical, not of small order and decodes (the
+// per-key tables of the throughput path, sv_kernels.hip) -- and table_A is
+// not built (the caller reads the key's cached table instead).
 SV_COLD bool sv_lat_pre(sv_lat& lat, const uint32_t A[8], const uint32_t R[8], const uint32_t S[8],
-                        const uint32_t hram[16], sv_u4* tabA, sv_u4* tabR, bool trivial = false) {
+                        const uint32_t hram[16], sv_u4* tabA, sv_u4* tabR, bool trivial = false,
+                        int a_status = -1) {
+#if SV_PREP_SEQ == 1
+  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(R) &&
+            (a_status >= 0 ? a_status != 0 : (sv_point_canonical(A) && !sv_small_order(A)));
+#else
+  // (the A/B variants always decode A: a cached table, if any, holds the same entries)
+  a_status = -1;
   bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
             sv_point_canonical(R);
+#endif
 #if SV_PREP_SEQ == 2
   // as below, with A and R through ONE copy of the decode + table code (a
   // rolled loop: the inlined exponentiation chain is ~30 KB of code per copy)
@@ -802,7 +814,7 @@ SV_COLD bool sv_lat_pre(sv_lat& lat, const uint32_t A[8], const uint32_t R[8], c
   // of -R, then the Euclid reduction with no point live
   uint32_t h[8];
   sc_reduce512(h, hram);
-  {
+  if (a_status < 0) {
     ge_p3 negA;
     ok = ge_frombytes(negA, A, true) && ok;
     sv_build_ltab(tabA, negA);
