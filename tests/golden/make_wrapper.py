@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generate tests/golden/wrapper.json: fixtures that pin the C++ mirror of the
+"""Generate tests/golden/wrapper.json (and derived.json): fixtures that pin the C++ mirror of the
 reference's signature WRAPPER logic, i.e. the layers above
 crypto_sign_verify_detached, against the reference's own tests:
 
@@ -24,8 +24,8 @@ crypto_sign_verify_detached, against the reference's own tests:
                     REQUIREs for the protocol versions it states.  Keys:
                     fromSeed(sha256(name)).  Contents hashes: sha256 of the case
                     name (the checker only signs/verifies the 32-byte hash).  The
-                    only "derived" cases are the missing-op-source cases that no
-                    reference test states (their source lines are cited).
+                    missing-op-source cases, which no reference test states, are
+                    written to derived.json instead (their source lines cited).
   value_sigs        src/herder/test/HerderTests.cpp:2052-2115: StellarValue
                     signatures (HerderImpl.cpp:2440-2449 verifies the node's
                     signature over xdr(networkID, ENVELOPE_TYPE_SCPVALUE, txSetHash,
@@ -468,10 +468,18 @@ def value_sigs():
 
 
 def main():
+    env = envelopes()
+    # reference-pinned cases only in wrapper.json; the cases no reference test
+    # states (their source lines cited) go to derived.json
     out = {"libsodium": "1.0.18", "pubkey_signature": pubkey_signature(), "hashx": hashx(),
-           "sign_tests": sign_tests(), "envelopes": envelopes(), "value_sigs": value_sigs()}
+           "sign_tests": sign_tests(), "envelopes": [c for c in env if not c["ref"].startswith("derived")],
+           "value_sigs": value_sigs()}
+    derived = {"libsodium": "1.0.18", "envelopes": [c for c in env if c["ref"].startswith("derived")]}
     with open(os.path.join(HERE, "wrapper.json"), "w") as f:
         json.dump(out, f, indent=0)
+    with open(os.path.join(HERE, "derived.json"), "w") as f:
+        json.dump(derived, f, indent=0)
+    print("derived.json: %d envelope cases" % len(derived["envelopes"]))
     print("wrapper.json: %d pubkey, %d hashx, %d sign, %d envelope cases, %d value signatures" % (
         len(out["pubkey_signature"]), len(out["hashx"]), len(out["sign_tests"]), len(out["envelopes"]),
         len(out["value_sigs"])))

@@ -26,6 +26,10 @@ import txset_gen as tg
 from conftest import GOLDEN, REPO
 
 WRAPPER = json.load(open(os.path.join(GOLDEN, "wrapper.json")))
+# cases no reference test states (missing operation source account, source
+# lines cited in each case's "ref"), kept apart from the reference-pinned ones
+DERIVED = json.load(open(os.path.join(GOLDEN, "derived.json")))
+ENVELOPES = WRAPPER["envelopes"] + DERIVED["envelopes"]
 
 
 @pytest.fixture(scope="module")
@@ -119,7 +123,7 @@ def _all_wrapper_checks(host, prefetch):
     ok, used = _run_txset(host, _hashx_rows(), prefetch)
     assert ok.all() and used.all(), "SignatureUtilsTest.cpp:34-48"
     assert _sign_test_calls(host) == [r["expect"] for r in WRAPPER["sign_tests"]], "CryptoTests.cpp:272-297"
-    for case in WRAPPER["envelopes"]:
+    for case in ENVELOPES:
         for proto, want in case["expect"].items():
             if not case.get("apply_only"):
                 _check_expect(_envelope_results(host, case, int(proto), prefetch), want,
@@ -155,7 +159,7 @@ def test_python_replay_matches_reference_outcomes(oracle):
         return oracle.oracle_ed25519_verify(sig, msg, len(msg), pk) == 0
 
     n = 0
-    for case in WRAPPER["envelopes"]:
+    for case in ENVELOPES:
         for proto, want in case["expect"].items():
             modes = ([] if case.get("apply_only") else [0]) + ([1] if proto == "21" else [])
             for mode in modes:
