@@ -52,33 +52,41 @@ void parallelFor(size_t n, size_t grain, F fn) {
 // or w0 + 1 bits, each rejection-sampled below the largest multiple of 2^w0
 // (2^(w0+1)) within the engine range, and the whole is rejected while >= the
 // range.
-size_t uniformIndex(std::minstd_rand& g, size_t lo, size_t hi) {
+// The draw's parameters depend only on (lo, hi), so they are computed once
+// (a cache draws over the same range for every eviction: the divisions below
+// were most of an eviction's cost).
+struct UniformDraw {
   using U = uint64_t;
-  const U r = (U)hi - (U)lo + 1;
-  if (r == 1) return lo;
-  const size_t Dt = 64;
-  size_t w;
-  if (r == 0) {
-    w = Dt;
-  } else {
-    w = Dt - (size_t)__builtin_clzll(r) - 1;
-    if ((r & (std::numeric_limits<U>::max() >> (Dt - w))) != 0) ++w;
-  }
-  const U R = (U)std::minstd_rand::max() - (U)std::minstd_rand::min() + 1;  // 2^31 - 2
-  const size_t m = 63 - (size_t)__builtin_clzll(R);                        // floor(log2 R) = 30
-  size_t n = w / m + (w % m != 0);
-  size_t w0 = w / n;
-  U y0 = w0 < Dt ? (R >> w0) << w0 : 0;
-  if (R - y0 > y0 / n) {
-    ++n;
+  static constexpr size_t Dt = 64;
+  size_t lo = 0, n = 0, n0 = 0, w0 = 0;
+  U r = 1, y0 = 0, y1 = 0, mask0 = 0, mask1 = 0;
+  UniformDraw() = default;
+  UniformDraw(size_t lo_, size_t hi) : lo(lo_) {
+    r = (U)hi - (U)lo + 1;
+    if (r == 1) return;
+    size_t w;
+    if (r == 0) {
+      w = Dt;
+    } else {
+      w = Dt - (size_t)__builtin_clzll(r) - 1;
+      if ((r & (std::numeric_limits<U>::max() >> (Dt - w))) != 0) ++w;
+    }
+    const U R = (U)std::minstd_rand::max() - (U)std::minstd_rand::min() + 1;  // 2^31 - 2
+    const size_t m = 63 - (size_t)__builtin_clzll(R);                        // floor(log2 R) = 30
+    n = w / m + (w % m != 0);
     w0 = w / n;
     y0 = w0 < Dt ? (R >> w0) << w0 : 0;
+    if (R - y0 > y0 / n) {
+      ++n;
+      w0 = w / n;
+      y0 = w0 < Dt ? (R >> w0) << w0 : 0;
+    }
+    n0 = n - w % n;
+    y1 = w0 < Dt - 1 ? (R >> (w0 + 1)) << (w0 + 1) : 0;
+    mask0 = w0 > 0 ? ~U(0) >> (Dt - w0) : U(0);
+    mask1 = w0 < Dt - 1 ? ~U(0) >> (Dt - (w0 + 1)) : ~U(0);
   }
-  const size_t n0 = n - w % n;
-  const U y1 = w0 < Dt - 1 ? (R >> (w0 + 1)) << (w0 + 1) : 0;
-  const U mask0 = w0 > 0 ? ~U(0) >> (Dt - w0) : U(0);
-  const U mask1 = w0 < Dt - 1 ? ~U(0) >> (Dt - (w0 + 1)) : ~U(0);
-  auto bits = [&]() -> U {
+  U bits(std::minstd_rand& g) const {
     U s = 0;
     for (size_t k = 0; k < n0; ++k) {
       U u;
@@ -97,15 +105,17 @@ size_t uniformIndex(std::minstd_rand& g, size_t lo, size_t hi) {
       s += u & mask1;
     }
     return s;
-  };
-  if (r == 0) return (size_t)bits();
-  U u;
-  do {
-    u = bits();
-  } while (u >= r);
-  return (size_t)(u + lo);
-}
-
+  }
+  size_t operator()(std::minstd_rand& g) const {
+    if (r == 1) return lo;
+    if (r == 0) return (size_t)bits(g);
+    U u;
+    do {
+      u = bits(g);
+    } while (u >= r);
+    return (size_t)(u + lo);
+  }
+};
 inline uint64_t keyBits(Hash const& h) {
   uint64_t v;
   std::memcpy(&v, h.data(), 8);  // keys are BLAKE2b outputs: uniformly distributed
@@ -115,7 +125,7 @@ inline uint64_t keyBits(Hash const& h) {
 // Restatement of RandomEvictionCache<Hash, bool>(maxSize, separatePRNG=true):
 // entries plus a vector of entry references in insertion order (the
 // reference's mValuePtrs); when over capacity, draw two positions of that
-// vector (uniformIndex above, the reference's rand_uniform), evict the less
+// vector (UniformDraw above, the reference's rand_uniform), evict the less
 // recently accessed entry and swap-remove its position.  get() and put() bump
 // a generation counter exactly as maybeGet()/put() do.
 //
@@ -146,7 +156,7 @@ class RandomEvictionCache {
     bool value;
   };
 
-  explicit RandomEvictionCache(size_t maxSize) : maxSize_(maxSize) {
+  explicit RandomEvictionCache(size_t maxSize) : maxSize_(maxSize), draw_(0, maxSize) {
     size_t cap = 16;
     while (cap < 2 * (maxSize + 1)) cap <<= 1;
     table_.assign(cap, 0u);
@@ -281,15 +291,15 @@ class RandomEvictionCache {
     table_[hole] = 0;
   }
   // Eviction draws are made ahead of time.  Every eviction happens at size
-  // maxSize + 1, so its two draws are uniformIndex(0, maxSize) -- the same
+  // maxSize + 1, so its two draws are UniformDraw(0, maxSize) -- the same
   // sequence sequential code would draw, just computed kAhead evictions early
   // so the victims' order-array entries and (half-way) their table slots can
   // be prefetched: an eviction otherwise waits on ~3 dependent cache misses.
   static constexpr size_t kAhead = 16;
   void drawAhead() {
     while (fcount_ < kAhead) {
-      const uint32_t a = (uint32_t)uniformIndex(rng_, 0, maxSize_);
-      const uint32_t b = (uint32_t)uniformIndex(rng_, 0, maxSize_);
+      const uint32_t a = (uint32_t)draw_(rng_);
+      const uint32_t b = (uint32_t)draw_(rng_);
       future_[(fhead_ + fcount_) % kAhead] = {a, b};
       ++fcount_;
       if (a < ordGen_.capacity() && b < ordGen_.capacity()) {
@@ -337,6 +347,7 @@ class RandomEvictionCache {
     ordGen_.pop_back();
   }
   size_t maxSize_;
+  UniformDraw draw_;  // uniform_int_distribution(0, maxSize_)
   size_t mask_;
   uint64_t generation_ = 0;
   std::vector<uint64_t> table_;
