@@ -131,6 +131,21 @@ int sv_ed25519_verify_batch_gather_cb(const uint8_t* const* pk, const uint8_t* c
                                       uint8_t* keys, void (*keys_ready)(void* ctx), void* ctx, const sv_opts* opts);
 
 /*
+ * As sv_ed25519_verify_batch_gather_cb, with the keys delivered in pieces:
+ * keys_ready(ctx, ready) runs with keys [0, ready) in `keys`, for increasing
+ * `ready`, the last time with ready == n.  For a one-chunk batch of >= 8192
+ * signatures the engine packs, copies up and hashes the batch in 4 pieces, so
+ * a caller that walks its cache in item order (verifySigBatch,
+ * /root/reference/src/crypto/SecretKey.cpp:446-466 per item) starts on the
+ * first quarter while the rest is still on its way.  Same threading rules.
+ */
+int sv_ed25519_verify_batch_gather_progress(const uint8_t* const* pk, const uint8_t* const* sig,
+                                            const uint8_t* const* msg, const uint32_t* msg_len, size_t n,
+                                            uint8_t* verdict, uint8_t* keys,
+                                            void (*keys_ready)(void* ctx, size_t ready), void* ctx,
+                                            const sv_opts* opts);
+
+/*
  * CPU path: the engine's own per-signature algorithm (csrc/verify_core.h,
  * the half-size equation of csrc/lattice.h) compiled for the host, on
  * `threads` threads (0: the machine's hardware concurrency, capped at 16).

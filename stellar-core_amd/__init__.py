@@ -65,6 +65,7 @@ EXPORTED_SYMBOLS = (
     "sv_ed25519_verify_batch_gather", "sv_ed25519_verify_batch_gather_cb", "sv_ed25519_verify_batch_cpu", "sv_ed25519_verify_cpu",
     "sv_set_device_map", "sv_set_min_shard", "sv_set_debug_flags", "sv_workspace_bytes", "sv_pinned_bytes",
     "sv_set_key_cache", "sv_key_cache_wait", "sv_key_cache_get_stats", "sv_set_key_tables",
+    "sv_ed25519_verify_batch_gather_progress",
 )
 
 # test knobs (include/stellar_sigverify.h sv_set_debug_flags)

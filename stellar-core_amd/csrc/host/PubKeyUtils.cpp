@@ -15,6 +15,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 
 #include "../../../include/stellar_sigverify.h"
 #include "../pool.h"
@@ -397,6 +398,9 @@ std::atomic<size_t> gCpuThreshold{1};
 const bool gTrace = getenv("SV_HOST_TRACE") != nullptr;  // stage timings of keyed batches to stderr
 
 using Item = PubKeyUtils::VerifyItem;
+// keyed batches at least this large walk the cache on the calling thread while
+// the engine call runs on a helper (verifySigBatch)
+constexpr size_t kThreadedWalkMin = 16384;
 
 // Per-thread scratch reused across calls: a large batch does not pay fresh
 // page faults for its index, key and pointer arrays every time.
@@ -473,21 +477,22 @@ void hostKeys(std::vector<Item> const& items, std::vector<size_t> const& rows, H
 // GPU engine over items[rows] (gather: the engine packs straight from the
 // items); keys != nullptr also returns the cache keys.  Returns the engine's
 // status; the caller falls back to the CPU path on any error.
-void runCallback(void* ctx) { (*static_cast<std::function<void()>*>(ctx))(); }
+void runProgress(void* ctx, size_t ready) { (*static_cast<std::function<void(size_t)>*>(ctx))(ready); }
 
-// keysReady (keyed passes): run once the keys are in `keys`; the engine calls
-// it while the GPU still verifies (one-chunk batches), else it runs here.
+// keysReady (keyed passes): keysReady(k) runs once keys [0, k) are in `keys`,
+// for increasing k up to n; the engine calls it while the GPU still verifies
+// (one-chunk batches, the keys in pieces), else it runs once here.
 int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, uint8_t* verdict, Hash* keys,
-              std::function<void()>* keysReady = nullptr) {
+              std::function<void(size_t)>* keysReady = nullptr, Scratch* scr = nullptr) {
   const size_t n = rows.size();
   static_assert(sizeof(Hash) == 32, "Hash must be 32 contiguous bytes");
   uint8_t* kb = reinterpret_cast<uint8_t*>(keys);
-  Scratch& st = scratch();
+  Scratch& st = scr ? *scr : scratch();  // (the caller's: this may run on a helper thread)
   if (keys) {
     if (PubKeyUtils::KeyedBatchVerifyFn tk = gTestKeyedVerifier.load()) {
       packForTestHook(items, rows, st);
       const int rc = tk(st.ppk.data(), st.psig.data(), st.pmsg.data(), st.poff.data(), st.plen.data(), n, verdict, kb);
-      if (rc == SV_OK && keysReady) (*keysReady)();
+      if (rc == SV_OK && keysReady) (*keysReady)(n);
       return rc;
     }
   } else if (PubKeyUtils::BatchVerifyFn tv = gTestVerifier.load()) {
@@ -506,8 +511,8 @@ int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, u
     st.len[i] = (uint32_t)it.msg.size();
   }
   if (keysReady)
-    return sv_ed25519_verify_batch_gather_cb(st.pk.data(), st.sig.data(), st.msg.data(), st.len.data(), n, verdict,
-                                             kb, runCallback, keysReady, nullptr);
+    return sv_ed25519_verify_batch_gather_progress(st.pk.data(), st.sig.data(), st.msg.data(), st.len.data(), n,
+                                                   verdict, kb, runProgress, keysReady, nullptr);
   return sv_ed25519_verify_batch_gather(st.pk.data(), st.sig.data(), st.msg.data(), st.len.data(), n, verdict, kb,
                                         nullptr);
 }
@@ -561,12 +566,15 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     pid.assign(E, kNone);
     uint64_t owner = 0;
     bool walked = false;
-    std::function<void()> phase1 = [&] {
+    size_t done = 0;  // items walked so far (the keys arrive in pieces)
+    std::function<void(size_t)> phase1 = [&](size_t ready) {
+      // (locked per piece: other callers' verifySig calls may fall between
+      // two pieces, as they may between two calls of a sequential loop)
       std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
-      owner = ++gBatchId;
-      for (size_t e = 0; e < E; ++e) {
-        if (e + 8 < E) gVerifySigCache.prefetch(keys[e + 8]);
-        if (e + 4 < E) gVerifySigCache.prefetchFound(keys[e + 4]);
+      if (done == 0) owner = ++gBatchId;
+      for (size_t e = done; e < ready; ++e) {
+        if (e + 8 < ready) gVerifySigCache.prefetch(keys[e + 8]);
+        if (e + 4 < ready) gVerifySigCache.prefetchFound(keys[e + 4]);
         const uint32_t id = gVerifySigCache.find(keys[e]);
         if (id != kNone) {
           auto const& ent = gVerifySigCache.at(id);
@@ -587,19 +595,47 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
         ++gVerifyCacheMiss;
         pid[e] = gVerifySigCache.insertNew(keys[e], false, owner, (uint32_t)e);
       }
-      walked = true;
+      done = ready;
+      if (done == E) walked = true;
     };
     const bool trace = gTrace;
     const auto tA = std::chrono::steady_clock::now();
     std::chrono::steady_clock::time_point tB{}, tC{};
-    std::function<void()> walk = phase1;
+    std::function<void(size_t)> walk = phase1;
     if (trace)
-      phase1 = [&] {
-        tB = std::chrono::steady_clock::now();
-        walk();
+      phase1 = [&](size_t ready) {
+        if (done == 0) tB = std::chrono::steady_clock::now();
+        walk(ready);
         tC = std::chrono::steady_clock::now();
       };
-    if (timedBatch(true, E, [&] { return gpuVerify(items, rows, verdict.data(), keys.data(), &phase1); }) == SV_OK) {
+    int erc;
+    if (E >= kThreadedWalkMin) {
+      // Large batches: the engine call runs on a helper thread and publishes
+      // how many keys are in (the engine delivers them in pieces); this thread
+      // walks the cache as they land -- the thread whose caches hold the
+      // verify cache from earlier calls.
+      std::atomic<size_t> ready{0};
+      std::atomic<bool> fin{false};
+      std::function<void(size_t)> publish = [&](size_t r) { ready.store(r, std::memory_order_release); };
+      std::thread eng([&] {
+        erc = timedBatch(true, E, [&] { return gpuVerify(items, rows, verdict.data(), keys.data(), &publish, &sc); });
+        fin.store(true, std::memory_order_release);
+      });
+      for (;;) {
+        const bool f = fin.load(std::memory_order_acquire);
+        const size_t r = ready.load(std::memory_order_acquire);
+        if (r > done) {
+          phase1(r);
+          continue;
+        }
+        if (f || done == E) break;
+        std::this_thread::yield();
+      }
+      eng.join();
+    } else {
+      erc = timedBatch(true, E, [&] { return gpuVerify(items, rows, verdict.data(), keys.data(), &phase1, &sc); });
+    }
+    if (erc == SV_OK) {
       gGpuSigs += E;
       gGpuBatches += 1;
       if (trace) {
@@ -612,11 +648,11 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
       ++gFallbacks;
       if (!walked) {
         hostKeys(items, rows, keys.data());
-        phase1();
+        phase1(E);  // (continues a walk the engine's pieces had started)
       }
       timedBatch(false, E, [&] { cpuVerify(items, rows, verdict.data()); return 0; });
     }
-    if (!walked) phase1();  // (not reached: the engine ran it on success)
+    if (!walked) phase1(E);  // (not reached: the engine ran it on success)
     const auto tE = std::chrono::steady_clock::now();
     resolvePending(pid.data(), verdict.data(), E, owner);
     if (trace)

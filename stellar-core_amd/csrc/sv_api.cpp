@@ -174,6 +174,7 @@ struct Stage {
   HostBuf h_in, h_out;
   DevBuf d_in, d_verdict, d_keys;
   hipEvent_t up = nullptr, done = nullptr, down = nullptr, keys_down = nullptr;
+  std::vector<hipEvent_t> pev;  // keys of piece k are down (one-chunk keyed batches)
   bool busy = false;  // a chunk's D2H is pending on `down`
   size_t lo = 0, m = 0;
 };
@@ -350,6 +351,8 @@ void release_device(Device& D) {
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.down) (void)hipEventDestroy(s.down);
     if (s.keys_down) (void)hipEventDestroy(s.keys_down);
+    for (hipEvent_t e : s.pev) (void)hipEventDestroy(e);
+    s.pev.clear();
     s.up = s.done = s.down = s.keys_down = nullptr;
   }
   D.msg.release(); D.off.release(); D.len.release(); D.keys.release(); D.h_sha.release();
@@ -640,8 +643,9 @@ Image image_of(const HostIn& in, size_t lo, size_t m, size_t* msg_total) {
   return im;
 }
 
-// Packs [lo, lo + m) into h (layout `im`), in parallel for large chunks.
-void pack(const HostIn& in, size_t lo, size_t m, const Image& im, uint8_t* h) {
+// Packing [lo, lo + m) into h (layout `im`): the message offsets first, then
+// rows [r0, r1) of the chunk, in parallel for large ranges.
+void pack_offsets(const HostIn& in, size_t lo, size_t m, const Image& im, uint8_t* h) {
   uint64_t* offs = (uint64_t*)(h + im.o_off);
   if (im.var) {
     uint64_t pos = 0;
@@ -650,10 +654,15 @@ void pack(const HostIn& in, size_t lo, size_t m, const Image& im, uint8_t* h) {
       pos += in.len[lo + i];
     }
   }
+}
+void pack_rows(const HostIn& in, size_t lo, size_t r0, size_t r1, const Image& im, uint8_t* h) {
+  const uint64_t* offs = (const uint64_t*)(h + im.o_off);
   const size_t kPart = 1u << 20;  // bytes per helper task
-  const size_t parts = std::max<size_t>(1, std::min<size_t>(pool().size() + 1, im.bytes / kPart));
+  const size_t m = r1 - r0;
+  const size_t est = im.bytes / std::max<size_t>(1, (im.o_sig / 32)) * m;  // (bytes of these rows, roughly)
+  const size_t parts = std::max<size_t>(1, std::min<size_t>(pool().size() + 1, est / kPart));
   pool().run(parts, [&](size_t t) {
-    const size_t a = m * t / parts, b = m * (t + 1) / parts;
+    const size_t a = r0 + m * t / parts, b = r0 + m * (t + 1) / parts;
     if (a == b) return;
     if (!in.gather()) {
       std::memcpy(h + 32 * a, in.pk + 32 * (lo + a), 32 * (b - a));
@@ -681,6 +690,30 @@ void pack(const HostIn& in, size_t lo, size_t m, const Image& im, uint8_t* h) {
     }
   });
 }
+void pack(const HostIn& in, size_t lo, size_t m, const Image& im, uint8_t* h) {
+  pack_offsets(in, lo, m, im, h);
+  pack_rows(in, lo, 0, m, im, h);
+}
+// H2D of rows [a, b) of a packed image (each section's slice); msg_total: the
+// image's message bytes.
+int upload_rows(const Image& im, size_t m, size_t a, size_t b, uint32_t fixed, size_t msg_total, const uint8_t* h,
+                uint8_t* d, hipStream_t st) {
+  SV_HIP(hipMemcpyAsync(d + 32 * a, h + 32 * a, 32 * (b - a), hipMemcpyHostToDevice, st));
+  SV_HIP(hipMemcpyAsync(d + im.o_sig + 64 * a, h + im.o_sig + 64 * a, 64 * (b - a), hipMemcpyHostToDevice, st));
+  size_t m0, m1;
+  if (im.var) {
+    SV_HIP(hipMemcpyAsync(d + im.o_off + 8 * a, h + im.o_off + 8 * a, 8 * (b - a), hipMemcpyHostToDevice, st));
+    SV_HIP(hipMemcpyAsync(d + im.o_len + 4 * a, h + im.o_len + 4 * a, 4 * (b - a), hipMemcpyHostToDevice, st));
+    const uint64_t* offs = (const uint64_t*)(h + im.o_off);
+    m0 = offs[a];
+    m1 = b < m ? offs[b] : msg_total;
+  } else {
+    m0 = a * (size_t)fixed;
+    m1 = b * (size_t)fixed;
+  }
+  if (m1 > m0) SV_HIP(hipMemcpyAsync(d + im.o_msg + m0, h + im.o_msg + m0, m1 - m0, hipMemcpyHostToDevice, st));
+  return SV_OK;
+}
 
 // SV_STAGE_TRACE: per-call host staging timings to stderr (developer knob)
 bool stage_trace() {
@@ -700,7 +733,62 @@ int drain_stage(Stage& s, uint8_t* verdict, uint8_t* keys) {
   return SV_OK;
 }
 
-typedef void (*KeysReadyFn)(void*);
+thread_local std::chrono::steady_clock::time_point g_trace_t0;  // (SV_STAGE_TRACE: host_slice entry)
+
+// Keys-ready notification of the keyed gather entry points: fn(ctx, ready)
+// with keys [0, ready) in the caller's array, called with increasing `ready`,
+// the last time with ready == n.
+struct KeysCb {
+  void (*fn)(void*, size_t) = nullptr;
+  void* ctx = nullptr;
+  explicit operator bool() const { return fn != nullptr; }
+  void operator()(size_t ready) const { fn(ctx, ready); }
+};
+// rows per piece of a one-chunk keyed batch whose keys go up in pieces (the
+// caller's walk starts on the first piece while later ones are packed,
+// copied and hashed)
+constexpr size_t kKeyPieces = 4, kKeyPieceMin = 8192;
+
+// Runs fn(0), fn(1), ... fn(P - 1) on a thread of its own, fn(k) once piece
+// k's events have been recorded (recorded(k + 1)); join() returns the first
+// error.  The destructor stops and joins it (an early error return of the
+// caller).
+class KeyNotifier {
+ public:
+  ~KeyNotifier() {
+    stop_.store(true);
+    if (th_.joinable()) th_.join();
+  }
+  void start(int dev, size_t P, std::function<int(size_t)> fn) {
+    fn_ = std::move(fn);
+    th_ = std::thread([this, dev, P] {
+      (void)hipSetDevice(dev);
+      for (size_t k = 0; k < P; ++k) {
+        while (rec_.load(std::memory_order_acquire) <= k) {
+          if (stop_.load()) return;
+          std::this_thread::yield();
+        }
+        const int rc = fn_(k);
+        if (rc != SV_OK) {
+          rc_ = rc;
+          return;
+        }
+      }
+    });
+  }
+  void recorded(size_t k) { rec_.store(k, std::memory_order_release); }
+  int join() {
+    if (th_.joinable()) th_.join();
+    return rc_;
+  }
+
+ private:
+  std::thread th_;
+  std::function<int(size_t)> fn_;
+  std::atomic<size_t> rec_{0};
+  std::atomic<bool> stop_{false};
+  int rc_ = SV_OK;
+};
 
 // Do the keys of a host batch repeat?  A sample of up to 4096 evenly spaced
 // rows: with s sampled of n and d repeats among them, K distinct keys give
@@ -738,7 +826,8 @@ bool repeated_keys(const HostIn& in, size_t n) {
 // are still running, so the caller's cache walk overlaps them; *cb_done
 // records that it ran.
 int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, int path,
-                      KeysReadyFn keys_cb, void* cb_ctx, bool* cb_done) {
+                      const KeysCb& kcb, bool* cb_done) {
+  KeyNotifier notifier;  // (joined on every return path)
   const size_t chunk = std::min(n, stage_chunk());
   int rc;
   const int ktm = kt_mode();
@@ -775,28 +864,71 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
       return rc;
     if (verdict && (rc = s.d_verdict.ensure(m))) return rc;
     if (keys && (rc = s.d_keys.ensure(32 * m))) return rc;
-    const auto t_pack = stage_trace() ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
-    pack(in, lo, m, im, (uint8_t*)s.h_in.p);
-    if (stage_trace()) g_trace_pack_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_pack).count();
-    SV_HIP(hipMemcpyAsync(s.d_in.p, s.h_in.p, im.bytes, hipMemcpyHostToDevice, up_s));
-    if (!single) {
-      SV_HIP(hipEventRecord(s.up, D.h2d));
-      SV_HIP(hipStreamWaitEvent(D.stream, s.up, 0));
-    }
     uint8_t* d = (uint8_t*)s.d_in.p;
+    uint8_t* hp = (uint8_t*)s.h_in.p;
     const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
     const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
-    if (keys)
-      SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m, s.d_keys.p,
-                            D.stream));
-    const bool early = single && keys_cb && keys && verdict;
-    if (early) {
-      // keys down on the D2H stream while the verify kernels run
-      SV_HIP(hipEventRecord(s.done, D.stream));
-      SV_HIP(hipStreamWaitEvent(D.d2h, s.done, 0));
-      SV_HIP(hipMemcpyAsync((uint8_t*)s.h_out.p + m, s.d_keys.p, 32 * m, hipMemcpyDeviceToHost, D.d2h));
-      SV_HIP(hipEventRecord(s.keys_down, D.d2h));
+    const bool early = single && kcb && keys && verdict;
+    // a one-chunk keyed batch with a keys-ready callback: pack, copy up, hash
+    // and copy the keys down in pieces, so the caller's walk starts early
+    const size_t P = early && m >= kKeyPieceMin ? kKeyPieces : 1;
+    while (s.pev.size() < P) {
+      hipEvent_t e;
+      SV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      s.pev.push_back(e);
     }
+    const auto t_pack = stage_trace() ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+    if (P == 1) {
+      pack(in, lo, m, im, hp);
+      SV_HIP(hipMemcpyAsync(s.d_in.p, s.h_in.p, im.bytes, hipMemcpyHostToDevice, up_s));
+      if (!single) {
+        SV_HIP(hipEventRecord(s.up, D.h2d));
+        SV_HIP(hipStreamWaitEvent(D.stream, s.up, 0));
+      }
+      if (keys)
+        SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m, s.d_keys.p,
+                              D.stream));
+      if (early) {
+        // keys down on the D2H stream while the verify kernels run
+        SV_HIP(hipEventRecord(s.done, D.stream));
+        SV_HIP(hipStreamWaitEvent(D.d2h, s.done, 0));
+        SV_HIP(hipMemcpyAsync((uint8_t*)s.h_out.p + m, s.d_keys.p, 32 * m, hipMemcpyDeviceToHost, D.d2h));
+        SV_HIP(hipEventRecord(s.pev[0], D.d2h));
+      }
+    } else {
+      // The pieces' keys go to the caller from a notifier thread while this
+      // thread packs and uploads the next pieces (every callback runs on that
+      // one thread, in order).
+      const auto t0 = g_trace_t0;
+      auto us = [t0] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(); };
+      notifier.start(D.phys, P, [&, m, lo](size_t k) -> int {
+        const size_t a = m * k / P, b = m * (k + 1) / P;
+        SV_HIP(hipEventSynchronize(s.pev[k]));
+        if (stage_trace()) fprintf(stderr, "SV_STAGE_TRACE keys piece %zu down at %.1f us\n", k, us());
+        std::memcpy(keys + 32 * (lo + a), (uint8_t*)s.h_out.p + m + 32 * a, 32 * (b - a));
+        kcb(lo + b);
+        if (stage_trace()) fprintf(stderr, "SV_STAGE_TRACE keys piece %zu walked at %.1f us\n", k, us());
+        return SV_OK;
+      });
+      pack_offsets(in, lo, m, im, hp);
+      if (stage_trace()) fprintf(stderr, "SV_STAGE_TRACE offsets at %.1f us\n", us());
+      for (size_t k = 0; k < P; ++k) {
+        const size_t a = m * k / P, b = m * (k + 1) / P;
+        pack_rows(in, lo, a, b, im, hp);
+        if ((rc = upload_rows(im, m, a, b, in.fixed, msg_total, hp, d, D.stream))) return rc;
+        SV_HIP(sv_launch_hash(0, D.grid * 2, d + 32 * a, d + im.o_sig + 64 * a,
+                              d + im.o_msg + (im.var ? 0 : a * (size_t)in.fixed), d_off ? d_off + a : nullptr,
+                              d_len ? d_len + a : nullptr, in.fixed, b - a, (uint8_t*)s.d_keys.p + 32 * a, D.stream));
+        SV_HIP(hipEventRecord(s.done, D.stream));
+        SV_HIP(hipStreamWaitEvent(D.d2h, s.done, 0));
+        SV_HIP(hipMemcpyAsync((uint8_t*)s.h_out.p + m + 32 * a, (uint8_t*)s.d_keys.p + 32 * a, 32 * (b - a),
+                              hipMemcpyDeviceToHost, D.d2h));
+        SV_HIP(hipEventRecord(s.pev[k], D.d2h));
+        notifier.recorded(k + 1);
+        if (stage_trace()) fprintf(stderr, "SV_STAGE_TRACE piece %zu enqueued at %.1f us\n", k, us());
+      }
+    }
+    if (stage_trace()) g_trace_pack_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_pack).count();
     if (verdict) {
       const int mode = im.var ? 1 : (in.fixed == 32 ? 0 : 2);
       if ((rc = launch_locked(D, mode, path, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m,
@@ -816,9 +948,13 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     s.lo = lo;
     s.m = m;
     if (early) {
-      SV_HIP(hipEventSynchronize(s.keys_down));
-      std::memcpy(keys + 32 * lo, ho + m, 32 * m);
-      keys_cb(cb_ctx);
+      if (P == 1) {
+        SV_HIP(hipEventSynchronize(s.pev[0]));
+        std::memcpy(keys + 32 * lo, ho + m, 32 * m);
+        kcb(lo + m);
+      } else if ((rc = notifier.join())) {
+        return rc;
+      }
       *cb_done = true;
     }
   }
@@ -828,14 +964,15 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
 }
 
 int host_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, int path,
-               KeysReadyFn keys_cb = nullptr, void* cb_ctx = nullptr, bool* cb_done = nullptr) {
+               const KeysCb& kcb = KeysCb(), bool* cb_done = nullptr) {
   std::lock_guard<std::mutex> g(D.mu);
   SV_HIP(hipSetDevice(D.phys));
   int rc;
   if ((rc = ready_locked(D))) return rc;
   const auto t0 = std::chrono::steady_clock::now();
+  g_trace_t0 = t0;
   g_trace_pack_us = 0;
-  rc = host_slice_locked(D, in, n, verdict, keys, path, keys_cb, cb_ctx, cb_done);
+  rc = host_slice_locked(D, in, n, verdict, keys, path, kcb, cb_done);
   if (stage_trace())
     fprintf(stderr, "SV_STAGE_TRACE n=%zu pack %.1f us total %.1f us\n", n, g_trace_pack_us,
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
@@ -1114,8 +1251,8 @@ bool lat_trace() {
 // One latency-bound host batch on the slot's latency lane: pinned image (+
 // the key slots when warm), one H2D, [hash kernel, keys D2H], the comb kernel
 // (every key cached) or the octet kernel, one D2H, one sync.
-int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, KeysReadyFn keys_cb,
-                     void* cb_ctx, bool* cb_done) {
+int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, const KeysCb& kcb,
+                     bool* cb_done) {
   LatLane& L = D.lat;
   int rc;
   if ((rc = lat_ready(D))) return rc;
@@ -1151,7 +1288,7 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
   const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
   uint8_t* ho = (uint8_t*)L.h_out.p;
-  const bool early = keys_cb && keys && verdict;
+  const bool early = kcb && keys && verdict;
   auto t_k = t_up;
   if (keys) {
     SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n, L.d_keys.p,
@@ -1186,7 +1323,7 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   if (early) {
     SV_HIP(hipEventSynchronize(L.keys_down));
     std::memcpy(keys, ho + n, 32 * n);
-    keys_cb(cb_ctx);
+    kcb(n);
     *cb_done = true;
   }
   lat_build(L);  // (after the verify work: a build waits for it on the device)
@@ -1210,11 +1347,11 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   return SV_OK;
 }
 
-int lat_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, KeysReadyFn keys_cb,
-              void* cb_ctx, bool* cb_done) {
+int lat_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, const KeysCb& kcb,
+              bool* cb_done) {
   std::lock_guard<std::mutex> g(D.lat.mu);
   SV_HIP(hipSetDevice(D.phys));
-  const int rc = lat_slice_locked(D, in, n, verdict, keys, keys_cb, cb_ctx, cb_done);
+  const int rc = lat_slice_locked(D, in, n, verdict, keys, kcb, cb_done);
   if (rc != SV_OK && D.lat.ready) (void)hipStreamSynchronize(D.lat.stream);  // nothing of this call in flight
   return rc;
 }
@@ -1329,10 +1466,10 @@ int debug_fail() {
 }
 
 int verify_host(const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, const sv_opts* opts,
-                KeysReadyFn keys_cb = nullptr, void* cb_ctx = nullptr) {
+                const KeysCb& kcb = KeysCb()) {
   if (n == 0) {
     int rc = check_opts(opts);
-    if (rc == SV_OK && keys_cb) keys_cb(cb_ctx);
+    if (rc == SV_OK && kcb) kcb(0);
     return rc;
   }
   if (!verdict && !keys) return fail(SV_ERR_INVALID_ARG, "null buffer");
@@ -1347,16 +1484,16 @@ int verify_host(const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, con
   if (devs.size() == 1) {
     // latency-bound batches (one latency launch) take the slot's latency lane
     if (resolve_path(path, n) == SV_PATH_LATENCY && n <= stage_chunk())
-      rc = lat_slice(*devs[0], in, n, verdict, keys, keys_cb, cb_ctx, &cb_done);
+      rc = lat_slice(*devs[0], in, n, verdict, keys, kcb, &cb_done);
     else
-      rc = host_slice(*devs[0], in, n, verdict, keys, path, keys_cb, cb_ctx, &cb_done);
+      rc = host_slice(*devs[0], in, n, verdict, keys, path, kcb, &cb_done);
   } else {
     rc = shard(devs, n, [&](Device& D, size_t lo, size_t hi) {
       return host_slice(D, in.sub(lo), hi - lo, verdict ? verdict + lo : nullptr, keys ? keys + 32 * lo : nullptr,
                         path);
     });
   }
-  if (rc == SV_OK && keys_cb && !cb_done) keys_cb(cb_ctx);  // (keys complete; no overlap possible)
+  if (rc == SV_OK && kcb && !cb_done) kcb(n);  // (keys complete; no overlap possible)
   return rc;
 }
 
@@ -1472,7 +1609,35 @@ int sv_ed25519_verify_batch_gather_cb(const uint8_t* const* pk, const uint8_t* c
   in.psig = sig;
   in.pmsg = msg;
   in.len = msg_len;
-  return verify_host(in, n, verdict, keys, opts, keys_ready, ctx);
+  struct Once {
+    void (*f)(void*);
+    void* c;
+    size_t n;
+  } once{keys_ready, ctx, n};
+  KeysCb kcb;
+  kcb.fn = [](void* p, size_t ready) {
+    const Once* o = static_cast<const Once*>(p);
+    if (ready == o->n) o->f(o->c);
+  };
+  kcb.ctx = &once;
+  return verify_host(in, n, verdict, keys, opts, kcb);
+}
+
+int sv_ed25519_verify_batch_gather_progress(const uint8_t* const* pk, const uint8_t* const* sig,
+                                            const uint8_t* const* msg, const uint32_t* msg_len, size_t n,
+                                            uint8_t* verdict, uint8_t* keys,
+                                            void (*keys_ready)(void* ctx, size_t ready), void* ctx,
+                                            const sv_opts* opts) {
+  if (n && (!pk || !verdict || !keys || !keys_ready)) return fail(SV_ERR_INVALID_ARG, "null buffer");
+  HostIn in;
+  in.ppk = pk;
+  in.psig = sig;
+  in.pmsg = msg;
+  in.len = msg_len;
+  KeysCb kcb;
+  kcb.fn = keys_ready;
+  kcb.ctx = ctx;
+  return verify_host(in, n, verdict, keys, opts, kcb);
 }
 
 int sv_ed25519_verify_batch_keyed(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
