@@ -30,6 +30,11 @@
 #ifndef SV_SHARE_T19
 #define SV_SHARE_T19 1
 #endif
+// p1p1 -> p3: Y is the g operand of both Y3 = Z Y and T3 = X Y, so its
+// 19-multiples are computed once as well (9 v_mul_lo_u32 per conversion)
+#ifndef SV_SHARE_Y19
+#define SV_SHARE_Y19 1
+#endif
 
 struct ge_p2 { fe X, Y, Z; };
 struct ge_p3 { fe X, Y, Z, T; };
@@ -66,54 +71,50 @@ SV_HD void ge_dbl(ge_p1p1& r, const fe& X, const fe& Y, const fe& Z) {
 #endif
 }
 
-// T is the g operand of two conversion products: its 19-multiples are
-// computed once (SV_SHARE_T19)
-SV_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
-#if SV_SHARE_T19
+// p1p1 -> p3 (wantT) or -> p2 (T left stale).  r must not alias p.  Bounds:
+// X (<= M5) and Z (<= M3) are only ever f operands; Y (<= M2) and T are the
+// g operands whose 19-multiples are shared: Y by Z Y and X Y, T by X T and
+// Z T.
+SV_HD void ge_p1p1_convert(ge_p3& r, const ge_p1p1& p, bool wantT) {
+#if SV_SHARE_T19 && SV_SHARE_Y19
+  {
+    fe19 y19;
+    fe_premul19(y19, p.Y);
+    if (wantT) fe_mul_g19(r.T, p.X, p.Y, y19);
+    fe_mul_g19(r.Y, p.Z, p.Y, y19);
+  }
+  fe19 t19;
+  fe_premul19(t19, p.T);
+  fe_mul_g19(r.X, p.X, p.T, t19);
+  fe_mul_g19(r.Z, p.Z, p.T, t19);
+#elif SV_SHARE_T19
+  if (wantT) fe_mul(r.T, p.X, p.Y);
   fe19 t19;
   fe_premul19(t19, p.T);
   fe_mul_g19(r.X, p.X, p.T, t19);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul_g19(r.Z, p.Z, p.T, t19);
 #else
+  if (wantT) fe_mul(r.T, p.X, p.Y);
   fe_mul(r.X, p.X, p.T);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
 #endif
 }
 
-SV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
-#if SV_SHARE_T19
-  fe19 t19;
-  fe_premul19(t19, p.T);
-  fe_mul_g19(r.X, p.X, p.T, t19);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul_g19(r.Z, p.Z, p.T, t19);
-#else
-  fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul(r.Z, p.Z, p.T);
-#endif
-  fe_mul(r.T, p.X, p.Y);
+SV_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
+  ge_p3 t;
+  ge_p1p1_convert(t, p, false);
+  r.X = t.X;
+  r.Y = t.Y;
+  r.Z = t.Z;
 }
+
+SV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) { ge_p1p1_convert(r, p, true); }
 
 // p1p1 -> p3 when the next step is an addition (wantT), else -> p2 (T left
-// stale).  wantT is wave-uniform, so this is a scalar branch.  Operand order
-// matters: p.X (up to M5 after a doubling) is always the f operand.
-SV_HD void ge_p1p1_to_p3_opt(ge_p3& r, const ge_p1p1& p, bool wantT) {
-  if (wantT) fe_mul(r.T, p.X, p.Y);
-#if SV_SHARE_T19
-  fe19 t19;
-  fe_premul19(t19, p.T);
-  fe_mul_g19(r.X, p.X, p.T, t19);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul_g19(r.Z, p.Z, p.T, t19);
-#else
-  fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul(r.Z, p.Z, p.T);
-#endif
-}
+// stale).  wantT is wave-uniform, so this is a scalar branch.
+SV_HD void ge_p1p1_to_p3_opt(ge_p3& r, const ge_p1p1& p, bool wantT) { ge_p1p1_convert(r, p, wantT); }
 
 // r = p + q where the caller has already swapped q's (Y+X, Y-X) pair for a
 // negative digit (by choosing load addresses); neg then only swaps the final

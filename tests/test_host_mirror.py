@@ -638,7 +638,7 @@ def test_cache_eviction_matches_sequential_reference(host, hostcore, keyed):
         out = np.zeros(len(order), np.uint8)
         pos = 0
         while pos < len(order):  # batches of varied sizes
-            size = int(rng.choice([1, 7, 1000, 4096, 333]))
+            size = int(rng.choice([1, 7, 1000, 4096, 333, 20000]))
             hi = min(len(order), pos + size)
             rc = host.svh_verify_sig_batch(P[pos:hi].ctypes.data_as(ctypes.c_void_p),
                                            np.ascontiguousarray(S[pos:hi]).ctypes.data_as(ctypes.c_void_p), None,

@@ -28,7 +28,7 @@ MASK = ["0x3ffffff" if w == 26 else "0x1ffffff" for w in WIDTH]
 CLOB = ", ".join('"v%d"' % r for r in range(0, 4)) + ", " + ", ".join('"s%d"' % r for r in range(88, 96))
 
 
-def product(name, terms_of_col, temps, inputs, doc, sig=None):
+def product(name, terms_of_col, temps, inputs, doc, sig=None, sconst=()):
     """terms_of_col[k] = list of (a_operand, b_operand) names; temps = list of
     (name, instruction text producing it); sig: explicit parameter list."""
     lines = []
@@ -63,7 +63,7 @@ def product(name, terms_of_col, temps, inputs, doc, sig=None):
     lines.append("v_alignbit_b32 %s, %s, %s, 26" % (oth[1], cur[2], cur[1]))
     lines.append("v_add_u32 %%[o1], %%[o1], %s" % oth[1])
     outs = ['[o%d] "=&v"(o[%d])' % (k, k) for k in range(10)] + ['[%s] "=&v"(%s)' % (n, n) for n, _ in temps]
-    ins = ['[%s] "v"(%s)' % (n, e) for n, e in inputs]
+    ins = ['[%s] "v"(%s)' % (n, e) for n, e in inputs] + ['[%s] "s"(%s)' % (n, e) for n, e in sconst]
     body = "\n".join('      "%s\\n"' % l for l in lines)
     out = []
     out.append("// %s" % doc)
@@ -120,40 +120,69 @@ def gen_mul(dbl, pre19=False):
     return product(name, cols, temps, inputs, doc)
 
 
+# Operand multiples a squaring derives (limb, multiplier), chosen by a small
+# integer program (minimum count of v_add_u32 / v_lshlrev_b32 / v_mul_lo_u32
+# such that every term f_i f_j (i <= j, factor 2 for i != j, 2 for odd * odd,
+# 19 for a wrapped column, 2 for DBL) is one product of two available 32-bit
+# operands within the input bound): 13 instead of 20 for fe_sq, 16 instead
+# of 30 for fe_sq2.
+SQ_DERIVED = {
+    # fe_sq: inputs <= M3 (even limbs 3 2^26, odd 3 2^25, + slack)
+    False: [(0, 2), (1, 2), (2, 2), (3, 2), (4, 2), (5, 2), (5, 38), (6, 19), (7, 2), (7, 38), (8, 2), (8, 19), (9, 38)],
+    # fe_sq2: inputs <= R (the doubling's Z, a product output)
+    True: [(0, 2), (0, 4), (1, 2), (1, 4), (2, 2), (3, 2), (3, 4), (4, 2), (5, 2), (5, 76), (6, 2), (6, 38), (7, 2),
+           (7, 76), (8, 38), (9, 76)],
+}
+SQ_BOUND = {False: (3 * 2**26 + 2**12, 3 * 2**25 + 2**12), True: (2**26 + 2**11, 2**25 + 2**17)}
+
+
+def limb_bound(i, bound):
+    return bound[i % 2]
+
+
 def gen_sq(dbl):
     inputs = [("f%d" % i, "f.v[%d]" % i) for i in range(10)]
+    bound = SQ_BOUND[dbl]
+    avail = {(i, 1): "f%d" % i for i in range(10)}
+    sconst = []
     temps = []
-    mult = {}  # (i, sh) -> operand name
-    for i in range(10):
-        mult[(i, 0)] = "f%d" % i
-    need = set()
+    for (i, m) in SQ_DERIVED[dbl]:  # (listed in derivation order)
+        assert m * limb_bound(i, bound) < 2**32, (i, m)
+        n = "m%d_%d" % (m, i)
+        if m % 2 == 0 and (i, m // 2) in avail:
+            src = avail[(i, m // 2)]
+            temps.append((n, "v_add_u32 %%[%s], %%[%s], %%[%s]" % (n, src, src)))
+        elif m & (m - 1) == 0:
+            temps.append((n, "v_lshlrev_b32 %%[%s], %d, %%[f%d]" % (n, m.bit_length() - 1, i)))
+        elif m <= 64:  # (an inline constant)
+            temps.append((n, "v_mul_lo_u32 %%[%s], %%[f%d], %d" % (n, i, m)))
+        else:  # VOP3 takes no literal: the constant comes in an SGPR
+            k = "k%d" % m
+            if (k, "%du" % m) not in sconst:
+                sconst.append((k, "%du" % m))
+            temps.append((n, "v_mul_lo_u32 %%[%s], %%[f%d], %%[%s]" % (n, i, k)))
+        avail[(i, m)] = n
+    cols = [[] for _ in range(10)]
     for i in range(10):
         for j in range(i, 10):
-            sh = (1 if i != j else 0) + (1 if (i % 2 and j % 2) else 0) + (1 if dbl else 0)
-            need.add((i, sh))
-    for sh in (1, 2, 3):
-        for i in range(10):
-            if any((i, s) in need for s in range(sh, 4)):
-                src = mult[(i, sh - 1)]
-                n = "d%d_%d" % (1 << sh, i)
-                temps.append((n, "v_add_u32 %%[%s], %%[%s], %%[%s]" % (n, src, src)))
-                mult[(i, sh)] = n
-    for j in range(5, 10):
-        temps.append(("t19_%d" % j, "v_mul_lo_u32 %%[t19_%d], %%[f%d], 19" % (j, j)))
-    cols = []
-    for k in range(10):
-        col = []
-        for i in range(10):
-            for j in range(i, 10):
-                if (i + j) % 10 != k:
-                    continue
-                sh = (1 if i != j else 0) + (1 if (i % 2 and j % 2) else 0) + (1 if dbl else 0)
-                b = "t19_%d" % j if i + j >= 10 else "f%d" % j
-                col.append((mult[(i, sh)], b))
-        cols.append(col)
+            k = (i + j) % 10
+            mult = (2 if i != j else 1) * (2 if (i % 2 and j % 2) else 1) * (19 if i + j >= 10 else 1) * (2 if dbl else 1)
+            pick = None
+            for (p, q) in ((i, j), (j, i)):
+                for (pp, a), an in sorted(avail.items()):
+                    if pp != p or mult % a:
+                        continue
+                    b = mult // a
+                    if (q, b) in avail:
+                        pick = (an, avail[(q, b)])
+                        break
+                if pick:
+                    break
+            assert pick, (i, j, mult)
+            cols[k].append(pick)
     name = "fe_sq2_asm" if dbl else "fe_sq_asm"
     doc = "h = %sf^2 (fe_sq_cm<%s>)" % ("2 " if dbl else "", "true" if dbl else "false")
-    return product(name, cols, temps, inputs, doc)
+    return product(name, cols, temps, inputs, doc, sconst=sconst)
 
 
 def main():
