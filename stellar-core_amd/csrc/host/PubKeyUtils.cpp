@@ -19,6 +19,7 @@
 
 #include "../../../include/stellar_sigverify.h"
 #include "../pool.h"
+#include "HostPool.h"
 #include "hashes.h"
 
 namespace stellar {
@@ -518,6 +519,15 @@ int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, u
 }
 
 }  // namespace
+
+void hostParallelFor(size_t n, size_t grain, std::function<void(size_t, size_t)> const& range) {
+  const size_t parts = std::max<size_t>(1, std::min<size_t>(hostPool().size() + 1, n / std::max<size_t>(1, grain)));
+  if (parts == 1) {
+    range(0, n);
+    return;
+  }
+  hostPool().run(parts, [&](size_t t) { range(n * t / parts, n * (t + 1) / parts); });
+}
 
 namespace PubKeyUtils {
 

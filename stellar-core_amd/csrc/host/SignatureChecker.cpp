@@ -7,6 +7,7 @@
 #include <cstring>
 #include <thread>
 
+#include "HostPool.h"
 #include "hashes.h"
 
 namespace stellar {
@@ -76,6 +77,7 @@ void SignatureBatchPrefetch::Storage::clear() {
   len.clear();
   verdict.clear();
   table.clear();
+  txBegin.clear();
 }
 
 SignatureBatchPrefetch::Storage& SignatureBatchPrefetch::spare() {
@@ -102,23 +104,6 @@ uint64_t SignatureBatchPrefetch::hashOf(const uint8_t* pk, const uint8_t* sig, c
   else if (len) std::memcpy(&c, msg, len);
   uint64_t h = a ^ (b * 0x9e3779b97f4a7c15ull) ^ ((c + len) * 0xc2b2ae3d27d4eb4full);
   return h ^ (h >> 29);
-}
-
-uint64_t SignatureBatchPrefetch::pushMsg(const uint8_t* msg, size_t msgLen) {
-  const uint64_t off = msg_.size();
-  msg_.resize(off + msgLen);
-  if (msgLen) std::memcpy(&msg_[off], msg, msgLen);
-  return off;
-}
-
-void SignatureBatchPrefetch::push(uint256 const& pk, Signature const& sig, uint64_t msgOff, size_t msgLen) {
-  const size_t i = len_.size();
-  pk_.resize(32 * (i + 1));
-  sig_.resize(64 * (i + 1));
-  std::memcpy(&pk_[32 * i], pk.data(), 32);
-  std::memcpy(&sig_[64 * i], sig.data(), 64);
-  off_.push_back(msgOff);
-  len_.push_back((uint32_t)msgLen);
 }
 
 namespace {
@@ -166,8 +151,9 @@ class InlineVec {
 };
 }  // namespace
 
-void SignatureBatchPrefetch::add(Hash const& contentsHash, std::vector<DecoratedSignature> const& signatures,
-                                 std::vector<Signer> const& signers) {
+void SignatureBatchPrefetch::enumerate(Storage& st, Hash const& contentsHash,
+                                       std::vector<DecoratedSignature> const& signatures,
+                                       std::vector<Signer> const& signers) {
   // The pairs SignatureChecker would verify, in its order per signature:
   // hint-matching ED25519 signers (SignatureUtils::verify) and
   // ED25519_SIGNED_PAYLOAD signers (verifyEd25519SignedPayload).  The
@@ -185,6 +171,21 @@ void SignatureBatchPrefetch::add(Hash const& contentsHash, std::vector<Decorated
     }
   }
   if (eds.empty()) return;
+  auto pushMsg = [&](const uint8_t* msg, size_t msgLen) {
+    const uint64_t off = st.msg.size();
+    st.msg.resize(off + msgLen);
+    if (msgLen) std::memcpy(&st.msg[off], msg, msgLen);
+    return off;
+  };
+  auto push = [&](uint256 const& pk, Signature const& sig, uint64_t msgOff, size_t msgLen) {
+    const size_t i = st.len.size();
+    st.pk.resize(32 * (i + 1));
+    st.sig.resize(64 * (i + 1));
+    std::memcpy(&st.pk[32 * i], pk.data(), 32);
+    std::memcpy(&st.sig[64 * i], sig.data(), 64);
+    st.off.push_back(msgOff);
+    st.len.push_back((uint32_t)msgLen);
+  };
   // message bytes are stored once per tx (contents hash) / per payload signer
   uint64_t hashOff = ~0ull;
   InlineVec<uint64_t, 48> payOff;
@@ -204,6 +205,75 @@ void SignatureBatchPrefetch::add(Hash const& contentsHash, std::vector<Decorated
       }
     }
   }
+}
+
+void SignatureBatchPrefetch::add(Hash const& contentsHash, std::vector<DecoratedSignature> const& signatures,
+                                 std::vector<Signer> const& signers) {
+  enumerate(st_, contentsHash, signatures, signers);
+}
+
+void SignatureBatchPrefetch::addBatch(std::vector<TxRef> const& txs) {
+  const size_t ntx = txs.size();
+  if (txBegin_.empty()) txBegin_.push_back((uint32_t)len_.size());
+  constexpr size_t kGrain = 256;
+  constexpr size_t kMaxParts = 16;
+  const size_t parts = std::min(kMaxParts, std::max<size_t>(1, ntx / kGrain));
+  if (parts == 1) {
+    for (auto const& t : txs) {
+      enumerate(st_, *t.contentsHash, *t.signatures, *t.signers);
+      txBegin_.push_back((uint32_t)len_.size());
+    }
+    return;
+  }
+  // phase 1: each part enumerates its range of txs into scratch of its own
+  // (kept per part across calls: no fresh page faults), recording the pair
+  // count after each tx; phase 2: the parts are copied into place in order.
+  static thread_local std::vector<Storage> tlScratch;
+  // (a local reference: a lambda names a thread_local directly, so inside the
+  // helpers tlScratch would be each helper thread's own, empty, instance)
+  std::vector<Storage>& scratch = tlScratch;
+  scratch.resize(kMaxParts);
+  std::vector<std::vector<uint32_t>> ends(parts);
+  hostParallelFor(parts, 1, [&](size_t a, size_t b) {
+    for (size_t p = a; p < b; ++p) {
+      Storage& s = scratch[p];
+      s.clear();
+      const size_t t0 = ntx * p / parts, t1 = ntx * (p + 1) / parts;
+      ends[p].clear();
+      for (size_t t = t0; t < t1; ++t) {
+        enumerate(s, *txs[t].contentsHash, *txs[t].signatures, *txs[t].signers);
+        ends[p].push_back((uint32_t)s.len.size());
+      }
+    }
+  });
+  std::vector<size_t> pairBase(parts + 1), msgBase(parts + 1);
+  pairBase[0] = len_.size();
+  msgBase[0] = msg_.size();
+  for (size_t p = 0; p < parts; ++p) {
+    pairBase[p + 1] = pairBase[p] + scratch[p].len.size();
+    msgBase[p + 1] = msgBase[p] + scratch[p].msg.size();
+  }
+  const size_t n = pairBase[parts];
+  pk_.resize(32 * n);
+  sig_.resize(64 * n);
+  off_.resize(n);
+  len_.resize(n);
+  msg_.resize(msgBase[parts]);
+  for (size_t p = 0; p < parts; ++p)
+    for (uint32_t e : ends[p]) txBegin_.push_back((uint32_t)(pairBase[p] + e));
+  hostParallelFor(parts, 1, [&](size_t a, size_t b) {
+    for (size_t p = a; p < b; ++p) {
+      Storage const& s = scratch[p];
+      const size_t m = s.len.size(), i0 = pairBase[p];
+      if (m) {
+        std::memcpy(&pk_[32 * i0], s.pk.data(), 32 * m);
+        std::memcpy(&sig_[64 * i0], s.sig.data(), 64 * m);
+        std::memcpy(&len_[i0], s.len.data(), 4 * m);
+        for (size_t k = 0; k < m; ++k) off_[i0 + k] = s.off[k] + msgBase[p];
+      }
+      if (!s.msg.empty()) std::memcpy(&msg_[msgBase[p]], s.msg.data(), s.msg.size());
+    }
+  });
 }
 
 void SignatureBatchPrefetch::buildTable() {
@@ -254,16 +324,27 @@ void SignatureBatchPrefetch::run(bool seedCache) {
   else buildTable();
 }
 
-bool SignatureBatchPrefetch::lookup(uint256 const& pk, Signature const& sig, ByteSlice const& msg,
-                                    bool& verdict) const {
-  if (table_.empty() || sig.size() != 64) return false;
+bool SignatureBatchPrefetch::lookup(uint256 const& pk, Signature const& sig, ByteSlice const& msg, bool& verdict,
+                                    size_t tx) const {
+  if (sig.size() != 64) return false;
+  auto same = [&](size_t i) {
+    return len_[i] == msg.size() && std::memcmp(&sig_[64 * i], sig.data(), 64) == 0 &&
+           std::memcmp(&pk_[32 * i], pk.data(), 32) == 0 &&
+           (msg.size() == 0 || std::memcmp(&msg_[off_[i]], msg.data(), msg.size()) == 0);
+  };
+  if (tx + 1 < txBegin_.size()) {  // the tx's own pairs, contiguous (addBatch)
+    for (size_t i = txBegin_[tx]; i < txBegin_[tx + 1]; ++i)
+      if (same(i)) {
+        verdict = verdict_[i] != 0;
+        return true;
+      }
+  }
+  if (table_.empty()) return false;
   for (size_t s = hashOf(pk.data(), sig.data(), msg.data(), msg.size()) & mask_;; s = (s + 1) & mask_) {
     const uint32_t t = table_[s];
     if (t == 0) return false;
     const size_t i = t - 1;
-    if (len_[i] == msg.size() && std::memcmp(&sig_[64 * i], sig.data(), 64) == 0 &&
-        std::memcmp(&pk_[32 * i], pk.data(), 32) == 0 &&
-        (msg.size() == 0 || std::memcmp(&msg_[off_[i]], msg.data(), msg.size()) == 0)) {
+    if (same(i)) {
       verdict = verdict_[i] != 0;
       return true;
     }
@@ -273,17 +354,18 @@ bool SignatureBatchPrefetch::lookup(uint256 const& pk, Signature const& sig, Byt
 // ---------------------------------------------------------------- checker
 SignatureChecker::SignatureChecker(uint32_t protocolVersion, Hash const& contentsHash,
                                    std::vector<DecoratedSignature> const& signatures,
-                                   SignatureBatchPrefetch const* prefetched)
+                                   SignatureBatchPrefetch const* prefetched, size_t prefetchTx)
     : mProtocolVersion(protocolVersion),
       mContentsHash(contentsHash),
       mSignatures(signatures),
       mUsedSignatures(signatures.size(), false),
-      mPrefetched(prefetched) {}
+      mPrefetched(prefetched),
+      mPrefetchTx(prefetchTx) {}
 
 bool SignatureChecker::verifyEd25519(DecoratedSignature const& sig, uint256 const& key, ByteSlice const& msg) const {
   if (mPrefetched && sig.signature.size() == 64) {
     bool v;
-    if (mPrefetched->lookup(key, sig.signature, msg, v)) return v;
+    if (mPrefetched->lookup(key, sig.signature, msg, v, mPrefetchTx)) return v;
   }
   PublicKey pk;
   pk.ed25519() = key;

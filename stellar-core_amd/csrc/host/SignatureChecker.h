@@ -79,19 +79,30 @@ class SignatureBatchPrefetch {
   // Enumerate the hint-matching ed25519 / signed-payload pairs of one tx.
   void add(Hash const& contentsHash, std::vector<DecoratedSignature> const& signatures,
            std::vector<Signer> const& signers);
+  // The same for a whole set of transactions, enumerated in parallel on the
+  // host pool (pairs in tx order, as add() per tx would give them).  The
+  // pairs of batch tx k are then also found by their position: a checker
+  // constructed with prefetchTx = k (the index in txs, counted over every
+  // addBatch call of this prefetch) searches them before the table.
+  struct TxRef {
+    Hash const* contentsHash;
+    std::vector<DecoratedSignature> const* signatures;
+    std::vector<Signer> const* signers;
+  };
+  void addBatch(std::vector<TxRef> const& txs);
   // One engine batch over everything added.  seedCache = false: the verdicts
   // go to the side table only (the engine is called directly, no cache
   // interaction); true: through PubKeyUtils::verifySigBatch, which also fills
   // the global verify cache (a later verifySig then hits).  An engine error
   // re-runs the batch on the CPU path.
   void run(bool seedCache = false);
-  // verdict for (pk, sig, msg) if prefetched
-  bool lookup(uint256 const& pk, Signature const& sig, ByteSlice const& msg, bool& verdict) const;
+  // verdict for (pk, sig, msg) if prefetched (tx: see addBatch)
+  static constexpr size_t kNoTx = ~size_t(0);
+  bool lookup(uint256 const& pk, Signature const& sig, ByteSlice const& msg, bool& verdict,
+              size_t tx = kNoTx) const;
   size_t pairs() const { return len_.size(); }
 
  private:
-  uint64_t pushMsg(const uint8_t* msg, size_t msgLen);
-  void push(uint256 const& pk, Signature const& sig, uint64_t msgOff, size_t msgLen);
   void buildTable();
   static constexpr size_t kAsyncTableMin = 4096;
   static uint64_t hashOf(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, size_t len);
@@ -100,9 +111,12 @@ class SignatureBatchPrefetch {
     std::vector<uint64_t> off;
     std::vector<uint32_t> len;
     std::vector<uint8_t> verdict;
-    std::vector<uint32_t> table;  // open addressing: pair index + 1, 0 = empty
+    std::vector<uint32_t> table;    // open addressing: pair index + 1, 0 = empty
+    std::vector<uint32_t> txBegin;  // addBatch: first pair of batch tx k (k + 1 entries)
     void clear();
   };
+  static void enumerate(Storage& st, Hash const& contentsHash, std::vector<DecoratedSignature> const& signatures,
+                        std::vector<Signer> const& signers);
   static Storage& spare();
   Storage st_;
   std::vector<uint8_t>& pk_ = st_.pk;
@@ -112,14 +126,18 @@ class SignatureBatchPrefetch {
   std::vector<uint32_t>& len_ = st_.len;
   std::vector<uint8_t>& verdict_ = st_.verdict;
   std::vector<uint32_t>& table_ = st_.table;
+  std::vector<uint32_t>& txBegin_ = st_.txBegin;
   size_t mask_ = 0;
 };
 
 class SignatureChecker {
  public:
+  // prefetchTx: the tx's index in the prefetch's addBatch order (its pairs
+  // are then found by position), or kNoTx
   SignatureChecker(uint32_t protocolVersion, Hash const& contentsHash,
                    std::vector<DecoratedSignature> const& signatures,
-                   SignatureBatchPrefetch const* prefetched = nullptr);
+                   SignatureBatchPrefetch const* prefetched = nullptr,
+                   size_t prefetchTx = SignatureBatchPrefetch::kNoTx);
   bool checkSignature(std::vector<Signer> const& signersV, int32_t neededWeight);
   bool checkAllSignaturesUsed() const;
 
@@ -131,6 +149,7 @@ class SignatureChecker {
   std::vector<DecoratedSignature> const& mSignatures;
   std::vector<bool> mUsedSignatures;
   SignatureBatchPrefetch const* mPrefetched;
+  size_t mPrefetchTx;
 };
 
 }  // namespace stellar

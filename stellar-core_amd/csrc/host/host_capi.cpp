@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <atomic>
 #include <exception>
 #include <future>
 #include <string>
@@ -14,6 +16,7 @@
 #include <vector>
 
 #include "../../../include/stellar_host.h"
+#include "HostPool.h"
 #include "PubKeyUtils.h"
 #include "SignatureChecker.h"
 #include "TransactionSignatures.h"
@@ -179,25 +182,50 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
     std::vector<Hash> hashes(ntx);
     std::vector<std::vector<DecoratedSignature>> dsigs(ntx);
     std::vector<std::vector<Signer>> sgn(ntx);
-    for (size_t t = 0; t < ntx; ++t) {
-      std::memcpy(hashes[t].data(), txs[t].contents_hash, 32);
-      dsigs[t] = sigRange(sigs, txs[t].sig_off, txs[t].nsigs);
-      for (uint32_t k = 0; k < txs[t].nsigners; ++k) sgn[t].push_back(signer(signers[txs[t].signer_off + k]));
-    }
+    // (the C structs -> the mirror's C++ objects, in parallel: a node already
+    // holds these objects; the tx set is independent per tx from here on)
+    std::atomic<bool> bad{false};
+    std::string err;
+    std::mutex errMu;
+    hostParallelFor(ntx, 256, [&](size_t a, size_t b) {
+      try {
+        for (size_t t = a; t < b; ++t) {
+          std::memcpy(hashes[t].data(), txs[t].contents_hash, 32);
+          dsigs[t] = sigRange(sigs, txs[t].sig_off, txs[t].nsigs);
+          sgn[t].reserve(txs[t].nsigners);
+          for (uint32_t k = 0; k < txs[t].nsigners; ++k) sgn[t].push_back(signer(signers[txs[t].signer_off + k]));
+        }
+      } catch (std::exception const& e) {
+        std::lock_guard<std::mutex> g(errMu);
+        bad = true;
+        err = e.what();
+      }
+    });
+    if (bad) throw std::invalid_argument(err);
     pc.lap("txset: marshal");
     SignatureBatchPrefetch pre;
     if (use_prefetch) {
-      for (size_t t = 0; t < ntx; ++t) pre.add(hashes[t], dsigs[t], sgn[t]);
+      std::vector<SignatureBatchPrefetch::TxRef> refs(ntx);
+      for (size_t t = 0; t < ntx; ++t) refs[t] = {&hashes[t], &dsigs[t], &sgn[t]};
+      pre.addBatch(refs);
       pc.lap("txset: prefetch add");
       pre.run(use_prefetch == 2);
       pc.lap("txset: prefetch run");
     }
     if (prefetched_pairs) *prefetched_pairs = pre.pairs();
-    for (size_t t = 0; t < ntx; ++t) {
-      SignatureChecker c(txs[t].protocol, hashes[t], dsigs[t], use_prefetch ? &pre : nullptr);
-      ok[t] = c.checkSignature(sgn[t], txs[t].needed_weight) ? 1 : 0;
-      all_used[t] = c.checkAllSignaturesUsed() ? 1 : 0;
-    }
+    auto check = [&](size_t a, size_t b) {
+      for (size_t t = a; t < b; ++t) {
+        SignatureChecker c(txs[t].protocol, hashes[t], dsigs[t], use_prefetch ? &pre : nullptr,
+                           use_prefetch ? t : SignatureBatchPrefetch::kNoTx);
+        ok[t] = c.checkSignature(sgn[t], txs[t].needed_weight) ? 1 : 0;
+        all_used[t] = c.checkAllSignaturesUsed() ? 1 : 0;
+      }
+    };
+    // With the pre-pass every checker only reads the side table, independent
+    // of the others: they run on the host pool.  Without it (the reference's
+    // flow: one verifySig per signature) they run in tx order on this thread.
+    if (use_prefetch) hostParallelFor(ntx, 128, check);
+    else check(0, ntx);
     pc.lap("txset: checkers");
     return SVH_OK;
   } catch (std::exception const& e) {

@@ -320,6 +320,30 @@ def test_signature_checker_matches_python_replay(host, engine, oracle):
     assert 0 < want_ok.sum() < len(txs) or want_ok.sum() == len(txs)
 
 
+def test_txset_prefetch_parallel_batch_matches_replay(host, engine, oracle):
+    """A set large enough that svh_check_txset enumerates the pairs in parallel
+    parts (SignatureBatchPrefetch::addBatch) and runs the checkers on the host
+    pool, each finding its pairs by position: outcomes equal the sequential
+    no-prefetch path and the Python replay."""
+    sign = _oracle_sign_fn(oracle)
+    txs = tg.generate(1500, sign, seed=23)
+    tg.add_payload_signatures(txs, sign)
+
+    def verify(pk, sig, msg):
+        return oracle.oracle_ed25519_verify(sig, msg, len(msg), pk) == 0
+
+    want_ok, want_used = tg.replay(txs, verify)
+    host.svh_cache_clear()
+    ok0, used0, _ = _check(host, txs, 0)
+    assert (ok0 == want_ok).all() and (used0 == want_used).all()
+    host.svh_cache_clear()
+    calls_before = engine.calls
+    ok1, used1, pairs = _check(host, txs, 1)
+    assert engine.calls - calls_before == 1
+    assert (ok1 == want_ok).all() and (used1 == want_used).all()
+    assert pairs > 0 and 0 < want_ok.sum() < len(txs)
+
+
 @pytest.mark.gpu
 def test_gpu_host_mirror_verify_sig(host, sv, golden):
     if sv.device_count() < 1:
