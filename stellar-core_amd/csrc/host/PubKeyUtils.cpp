@@ -172,6 +172,13 @@ class RandomEvictionCache {
     rng_.seed(seed);
     fcount_ = 0;  // the queued draws came from the old seed
   }
+  // Queues the draws of up to `evictions` future evictions (at most as many
+  // as `items` inserts could cause); returns how many are queued.
+  size_t preDraw(size_t evictions) {
+    drawAhead(std::min(evictions, fcount_ + 4096));
+    return fcount_;
+  }
+  size_t queuedDraws() const { return fcount_; }
   void prefetch(Hash const& k) const { __builtin_prefetch(&table_[keyBits(k) & mask_]); }
   // second stage of the walk's prefetch (the slot of k was prefetched a few
   // items earlier): the entry of the first slot whose tag matches k
@@ -294,36 +301,49 @@ class RandomEvictionCache {
   }
   // Eviction draws are made ahead of time.  Every eviction happens at size
   // maxSize + 1, so its two draws are UniformDraw(0, maxSize) -- the same
-  // sequence sequential code would draw, just computed kAhead evictions early
-  // so the victims' order-array entries and (half-way) their table slots can
-  // be prefetched: an eviction otherwise waits on ~3 dependent cache misses.
+  // sequence sequential code would draw, just computed early: at least kAhead
+  // evictions ahead (so the victims' order-array entries and, half-way,
+  // their table slots can be prefetched), or many more when a large batch
+  // pre-draws while it waits for its keys (preDraw).  Queued draws belong to
+  // the future whatever happens in between (the sequence never depends on
+  // the cache's contents); maybeSeed drops them.
   static constexpr size_t kAhead = 16;
-  void drawAhead() {
-    while (fcount_ < kAhead) {
+  void drawAhead(size_t want) {
+    while (fcount_ < want) {
       const uint32_t a = (uint32_t)draw_(rng_);
       const uint32_t b = (uint32_t)draw_(rng_);
-      future_[(fhead_ + fcount_) % kAhead] = {a, b};
-      ++fcount_;
-      if (a < ordGen_.capacity() && b < ordGen_.capacity()) {
-        __builtin_prefetch(ordGen_.data() + a);
-        __builtin_prefetch(ordGen_.data() + b);
-        __builtin_prefetch(ordTag_.data() + a);
-        __builtin_prefetch(ordTag_.data() + b);
-        __builtin_prefetch(ordId_.data() + a);
-        __builtin_prefetch(ordId_.data() + b);
+      if (fcount_ == future_.size()) {  // grow the ring (unwrapping it)
+        std::vector<std::pair<uint32_t, uint32_t>> g(std::max<size_t>(64, 2 * future_.size()));
+        for (size_t k = 0; k < fcount_; ++k) g[k] = future_[(fhead_ + k) % future_.size()];
+        future_.swap(g);
+        fhead_ = 0;
       }
+      future_[(fhead_ + fcount_) % future_.size()] = {a, b};
+      ++fcount_;
     }
   }
+  std::pair<uint32_t, uint32_t> const& futureAt(size_t k) const { return future_[(fhead_ + k) % future_.size()]; }
   void evictOne() {
     const size_t sz = ordId_.size();
     if (sz == 0) return;
-    drawAhead();
-    const size_t ia = future_[fhead_].first, ib = future_[fhead_].second;
-    fhead_ = (fhead_ + 1) % kAhead;
+    drawAhead(kAhead + 1);
+    const size_t ia = futureAt(0).first, ib = futureAt(0).second;
+    fhead_ = (fhead_ + 1) % future_.size();
     --fcount_;
+    {  // kAhead ahead: the candidates' order-array entries
+      auto const& f = futureAt(kAhead - 1);
+      if (f.first < ordGen_.capacity() && f.second < ordGen_.capacity()) {
+        __builtin_prefetch(ordGen_.data() + f.first);
+        __builtin_prefetch(ordGen_.data() + f.second);
+        __builtin_prefetch(ordTag_.data() + f.first);
+        __builtin_prefetch(ordTag_.data() + f.second);
+        __builtin_prefetch(ordId_.data() + f.first);
+        __builtin_prefetch(ordId_.data() + f.second);
+      }
+    }
     {  // half-way ahead: the candidate victims' table slots and entries (the
        // victim's entry is rewritten by the next insert)
-      auto const& f = future_[(fhead_ + kAhead / 2) % kAhead];
+      auto const& f = futureAt(kAhead / 2);
       __builtin_prefetch(&table_[ordTag_[f.first] & mask_]);
       __builtin_prefetch(&table_[ordTag_[f.second] & mask_]);
       if (f.first < ordId_.size() && f.second < ordId_.size()) {
@@ -331,7 +351,6 @@ class RandomEvictionCache {
         __builtin_prefetch(&entries_[ordId_[f.second]], 1);
       }
     }
-    drawAhead();
     const size_t iv = ordGen_[ia] < ordGen_[ib] ? ia : ib;
     const uint32_t victim = ordId_[iv];
     eraseSlot(ordTag_[iv], victim);
@@ -358,7 +377,7 @@ class RandomEvictionCache {
   std::vector<uint32_t> ordId_, ordTag_;
   std::vector<uint64_t> ordGen_;
   std::minstd_rand rng_;  // stellar_default_random_engine, src/util/Math.h:26
-  std::pair<uint32_t, uint32_t> future_[kAhead];
+  std::vector<std::pair<uint32_t, uint32_t>> future_;  // ring of queued draws
   size_t fhead_ = 0, fcount_ = 0;
 };
 
@@ -577,11 +596,43 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     uint64_t owner = 0;
     bool walked = false;
     size_t done = 0;  // items walked so far (the keys arrive in pieces)
+    // verdictsIn: the engine call has returned, so a miss can be inserted
+    // with its verdict (no pending state, nothing left for resolvePending)
+    bool verdictsIn = false;
+    size_t pendEnd = E;  // items [0, pendEnd) may hold pending inserts
     std::function<void(size_t)> phase1 = [&](size_t ready) {
       // (locked per piece: other callers' verifySig calls may fall between
       // two pieces, as they may between two calls of a sequential loop)
       std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
       if (done == 0) owner = ++gBatchId;
+      if (verdictsIn) {
+        pendEnd = std::min(pendEnd, done);
+        for (size_t e = done; e < ready; ++e) {
+          if (e + 8 < ready) gVerifySigCache.prefetch(keys[e + 8]);
+          if (e + 4 < ready) gVerifySigCache.prefetchFound(keys[e + 4]);
+          const uint32_t id = gVerifySigCache.find(keys[e]);
+          if (id != kNone) {
+            auto const& ent = gVerifySigCache.at(id);
+            if (ent.owner == 0 || ent.owner == owner) {
+              ++gVerifyCacheHit;
+              auto& t = gVerifySigCache.touch(id);
+              if (t.owner == 0) {
+                hit[e] = 1;
+                out[rows[e]] = t.value;
+              }
+              continue;
+            }
+            ++gVerifyCacheMiss;
+            gVerifySigCache.update(id, verdict[e] != 0, 0, 0);
+            continue;
+          }
+          ++gVerifyCacheMiss;
+          gVerifySigCache.insertNew(keys[e], verdict[e] != 0, 0, 0);
+        }
+        done = ready;
+        if (done == E) walked = true;
+        return;
+      }
       for (size_t e = done; e < ready; ++e) {
         if (e + 8 < ready) gVerifySigCache.prefetch(keys[e + 8]);
         if (e + 4 < ready) gVerifySigCache.prefetchFound(keys[e + 4]);
@@ -631,14 +682,27 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
         erc = timedBatch(true, E, [&] { return gpuVerify(items, rows, verdict.data(), keys.data(), &publish, &sc); });
         fin.store(true, std::memory_order_release);
       });
+      size_t drawn = 0;
       for (;;) {
         const bool f = fin.load(std::memory_order_acquire);
         const size_t r = ready.load(std::memory_order_acquire);
         if (r > done) {
-          phase1(r);
+          // (once the engine has returned, every verdict is in `verdict`;
+          // walked in slices so the switch happens as soon as it has)
+          if (f && erc == SV_OK) verdictsIn = true;
+          phase1(std::min(r, done + 8192));
           continue;
         }
         if (f || done == E) break;
+        if (drawn < E - done) {
+          // waiting for keys: queue the eviction draws the walk may need
+          // (at most one per remaining item), a slice per lock hold
+          std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
+          const size_t before = gVerifySigCache.queuedDraws();
+          drawn = gVerifySigCache.preDraw(E - done);
+          if (drawn == before) drawn = E;  // (nothing more to queue)
+          continue;
+        }
         std::this_thread::yield();
       }
       eng.join();
@@ -664,7 +728,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     }
     if (!walked) phase1(E);  // (not reached: the engine ran it on success)
     const auto tE = std::chrono::steady_clock::now();
-    resolvePending(pid.data(), verdict.data(), E, owner);
+    resolvePending(pid.data(), verdict.data(), pendEnd, owner);
     if (trace)
       fprintf(stderr, "[verifySigBatch keyed n=%zu] resolve %.3f ms\n", E,
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tE).count());

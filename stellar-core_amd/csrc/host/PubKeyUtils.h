@@ -51,8 +51,54 @@ struct PublicKey {
   uint256 const& ed25519() const { return key_; }
 };
 
-// XDR Signature = opaque<64>
-using Signature = std::vector<uint8_t>;
+// XDR Signature = opaque<64>, held inline: at most 64 bytes, so a tx set's
+// ~30k decorated signatures cost no heap allocation each (xdrpp's
+// opaque_vec<64> is a std::vector).  The vector operations the mirror uses.
+class Signature {
+ public:
+  static constexpr size_t kMax = 64;
+  Signature() = default;
+  explicit Signature(size_t n) { resize(n); }
+  template <class It>
+  Signature(It first, It last) {
+    assign(first, last);
+  }
+  template <class It>
+  void assign(It first, It last) {
+    size_t n = 0;
+    for (It it = first; it != last; ++it) {
+      if (n == kMax) throw std::length_error("Signature: more than 64 bytes (XDR opaque<64>)");
+      buf_[n++] = (uint8_t)*it;
+    }
+    n_ = (uint8_t)n;
+  }
+  void resize(size_t n) {
+    if (n > kMax) throw std::length_error("Signature: more than 64 bytes (XDR opaque<64>)");
+    for (size_t k = n_; k < n; ++k) buf_[k] = 0;
+    n_ = (uint8_t)n;
+  }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  uint8_t* data() { return buf_; }
+  const uint8_t* data() const { return buf_; }
+  uint8_t* begin() { return buf_; }
+  uint8_t* end() { return buf_ + n_; }
+  const uint8_t* begin() const { return buf_; }
+  const uint8_t* end() const { return buf_ + n_; }
+  uint8_t& operator[](size_t i) { return buf_[i]; }
+  uint8_t operator[](size_t i) const { return buf_[i]; }
+  bool operator==(Signature const& o) const {
+    if (n_ != o.n_) return false;
+    for (size_t k = 0; k < n_; ++k)
+      if (buf_[k] != o.buf_[k]) return false;
+    return true;
+  }
+  bool operator!=(Signature const& o) const { return !(*this == o); }
+
+ private:
+  uint8_t buf_[kMax] = {};
+  uint8_t n_ = 0;
+};
 
 // Non-owning (pointer, size), src/crypto/ByteSlice.h:19-80
 struct ByteSlice {

@@ -92,6 +92,9 @@ void svh_sha256(uint8_t out[32], const uint8_t* p, size_t n) {
 
 int svh_verify_sig(const uint8_t pk[32], const uint8_t* sig, size_t sig_len, const uint8_t* msg, size_t msg_len) {
   try {
+    // (verifySig rejects any size but 64 before touching the cache,
+    // SecretKey.cpp:441-444; an XDR opaque<64> cannot hold more)
+    if (sig_len > Signature::kMax) return 0;
     PublicKey k;
     std::memcpy(k.ed25519().data(), pk, 32);
     Signature s(sig, sig + sig_len);

@@ -744,10 +744,11 @@ struct KeysCb {
   explicit operator bool() const { return fn != nullptr; }
   void operator()(size_t ready) const { fn(ctx, ready); }
 };
-// rows per piece of a one-chunk keyed batch whose keys go up in pieces (the
-// caller's walk starts on the first piece while later ones are packed,
-// copied and hashed)
-constexpr size_t kKeyPieces = 4, kKeyPieceMin = 8192;
+// A one-chunk keyed batch of at least kKeyPieceMin rows sends its keys up in
+// pieces of about kKeyPieceRows (at most kKeyPiecesMax pieces): the caller's
+// cache walk starts on the first piece while later ones are packed, copied
+// and hashed (the walk, ~30 ns per row, is the slower side).
+constexpr size_t kKeyPieceRows = 8192, kKeyPieceMin = 8192, kKeyPiecesMax = 16;
 
 // Runs fn(0), fn(1), ... fn(P - 1) on a thread of its own, fn(k) once piece
 // k's events have been recorded (recorded(k + 1)); join() returns the first
@@ -871,7 +872,8 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     const bool early = single && kcb && keys && verdict;
     // a one-chunk keyed batch with a keys-ready callback: pack, copy up, hash
     // and copy the keys down in pieces, so the caller's walk starts early
-    const size_t P = early && m >= kKeyPieceMin ? kKeyPieces : 1;
+    const size_t P =
+        early && m >= kKeyPieceMin ? std::min(kKeyPiecesMax, std::max<size_t>(2, (m + kKeyPieceRows - 1) / kKeyPieceRows)) : 1;
     while (s.pev.size() < P) {
       hipEvent_t e;
       SV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
