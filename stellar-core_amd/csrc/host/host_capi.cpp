@@ -283,14 +283,20 @@ int svh_check_envelopes(const svh_envelope* env, size_t n, const svh_decorated_s
     }
     if (prefetched_pairs) *prefetched_pairs = pre.pairs();
     SignatureBatchPrefetch const* p = prefetch ? &pre : nullptr;
-    for (size_t t = 0; t < n; ++t) {
-      TxSigResult r = env[t].fee_bump ? checkFeeBumpSignatures(txs[t], snap, protocol, p, for_apply != 0)
-                                      : checkTransactionSignatures(txs[t].inner, snap, protocol, p, for_apply != 0);
-      results[t].code = r.code;
-      results[t].inner_code = r.innerCode;
-      results[t].failed_op = r.failedOp;
-      results[t].op_code = r.opCode;
-    }
+    auto check = [&](size_t a, size_t b) {
+      for (size_t t = a; t < b; ++t) {
+        TxSigResult r = env[t].fee_bump ? checkFeeBumpSignatures(txs[t], snap, protocol, p, for_apply != 0)
+                                        : checkTransactionSignatures(txs[t].inner, snap, protocol, p, for_apply != 0);
+        results[t].code = r.code;
+        results[t].inner_code = r.innerCode;
+        results[t].failed_op = r.failedOp;
+        results[t].op_code = r.opCode;
+      }
+    };
+    // (as svh_check_txset: with the pre-pass the checkers only read the side
+    // table and the account snapshot, so they run on the host pool)
+    if (prefetch) hostParallelFor(n, 128, check);
+    else check(0, n);
     return SVH_OK;
   } catch (std::exception const& e) {
     return guard_exc(e);
