@@ -1,7 +1,11 @@
-"""N>1 path on CPU: world_size-2 gloo ranks shard one batch into contiguous
-slices (stellar-core_amd/sharding.py, the partition bench.py and the C-ABI
-use), verify their slice with the oracle as a stand-in for the GPU, gather the
-verdict bytes and must reproduce the single-process verdicts and digest."""
+"""N>1 path: world_size-2 gloo ranks shard one batch into contiguous slices
+(stellar-core_amd/sharding.py, the partition bench.py and the C-ABI use),
+verify their slice through the product library's CPU path
+(sv_ed25519_verify_batch_cpu: the engine's own algorithm built for the host;
+engine="gpu" takes sv_ed25519_verify_batch instead, which torchrun-launched
+ranks use on GPU nodes -- never spawned from a test process that already
+holds the GPU), gather the verdict bytes and must reproduce the libsodium
+verdicts and their digest."""
 import importlib
 import os
 import socket
@@ -25,24 +29,35 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, rows, q):
+def _rank_main(rank, world, port, rows, q, engine="cpu"):
     sys.path.insert(0, REPO)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import ctypes
     sh = importlib.import_module("stellar-core_amd.sharding")
-    oracle = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+    lib = ctypes.CDLL(os.path.join(REPO, "stellar-core_amd", "libstellar_sigverify.so"))
     d = load_golden("adversarial")
     n = len(rows)
     lo, hi = sh.shard_bounds(n, world, rank)
-    local = []
-    for i in rows[lo:hi]:
-        o, ln = int(d["msg_off"][i]), int(d["msg_len"][i])
-        ok = oracle.oracle_ed25519_verify(d["sig"][i].tobytes(), d["msg"][o:o + ln].tobytes(),
-                                          ctypes.c_size_t(ln), d["pk"][i].tobytes()) == 0
-        local.append(1 if ok else 0)
-    full = sh.gather_verdicts(np.array(local, np.uint8), n, world, rank)
+    mine = rows[lo:hi]
+    m = len(mine)
+    pk = np.ascontiguousarray(d["pk"][mine])
+    sig = np.ascontiguousarray(d["sig"][mine])
+    ln = d["msg_len"][mine].astype(np.uint32)
+    off = np.zeros(m, np.uint64)
+    if m:
+        off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    msg = np.frombuffer(b"".join(d["msg"][int(d["msg_off"][i]):int(d["msg_off"][i]) + int(d["msg_len"][i])].tobytes()
+                                 for i in mine) + b"\0", np.uint8)
+    local = np.zeros(m, np.uint8)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    if engine == "gpu":
+        rc = lib.sv_ed25519_verify_batch(P(pk), P(sig), P(msg), P(off), P(ln), ctypes.c_size_t(m), P(local), None)
+    else:
+        rc = lib.sv_ed25519_verify_batch_cpu(P(pk), P(sig), P(msg), P(off), P(ln), ctypes.c_size_t(m), P(local), 1)
+    assert rc == 0, rc
+    full = sh.gather_verdicts(local, n, world, rank)
     if rank == 0:
         q.put((full.tolist(), sh.verdict_digest(full)))
         q.close()
@@ -63,15 +78,11 @@ def test_shard_bounds_partition():
             assert max(h - lo for lo, h in b) - min(h - lo for lo, h in b) <= 1
 
 
-@pytest.mark.parametrize("world", [2])
-def test_gloo_world2_gather_matches_single_process(world):
-    d = load_golden("adversarial")
-    rng = np.random.default_rng(0)
-    rows = np.sort(rng.choice(len(d["verdict"]), 61, replace=False))  # odd size: ragged shards
+def _run_world(world, rows, engine):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, rows, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, rows, q, engine)) for r in range(world)]
     for p in procs:
         p.daemon = True  # never joined at interpreter exit
         p.start()
@@ -86,6 +97,15 @@ def test_gloo_world2_gather_matches_single_process(world):
                 p.kill()
                 p.join(5)
     assert codes == [0] * world, codes
+    return full, digest
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_world2_gather_matches_single_process(world):
+    d = load_golden("adversarial")
+    rng = np.random.default_rng(0)
+    rows = np.sort(rng.choice(len(d["verdict"]), 61, replace=False))  # odd size: ragged shards
+    full, digest = _run_world(world, rows, "cpu")
     sh = importlib.import_module("stellar-core_amd.sharding")
     want = d["verdict"][rows]
     assert np.array_equal(np.array(full, np.uint8), want)
