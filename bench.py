@@ -476,7 +476,9 @@ def main():
         achieved = kernel_rate * W_MAD_PER_VERIFY / 1e12
         traffic = None
         prof = {}
-        tf = os.path.join(REPO, "profiles", "r02_traffic.json")
+        tf = os.path.join(REPO, "profiles", "r03_traffic.json")
+        if not os.path.exists(tf):
+            tf = os.path.join(REPO, "profiles", "r02_traffic.json")
         if os.path.exists(tf):
             try:
                 with open(tf) as f:
@@ -486,7 +488,7 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
                     prof = {k: tj[k] for k in ("valu_inst_per_verify", "valu_issue_util", "l2_hit_rate",
                                                "kernel_avg_ns") if k in tj}
-                    prof["source"] = "profiles/r02_traffic.json (rocprofv3 PMC, tools/profile_run.sh)"
+                    prof["source"] = "profiles/%s (rocprofv3 PMC, tools/profile_run.sh)" % os.path.basename(tf)
             except Exception:
                 traffic = None
         # hardware multiply-adds the SIMDs issue per verify (tools/madcount.py,
