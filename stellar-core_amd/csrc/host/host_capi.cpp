@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <atomic>
 #include <exception>
@@ -42,6 +43,23 @@ thread_local std::string t_err;
 int guard_exc(std::exception const& e) {
   t_err = e.what();
   return SVH_ERR_INVALID_ARG;
+}
+
+// hostParallelFor whose pieces may throw: the first exception is rethrown on
+// this thread once every piece has returned (an exception must not leave a
+// pool thread)
+void parallelOrThrow(size_t n, size_t grain, std::function<void(size_t, size_t)> const& range) {
+  std::exception_ptr first;
+  std::mutex mu;
+  hostParallelFor(n, grain, [&](size_t a, size_t b) {
+    try {
+      range(a, b);
+    } catch (...) {
+      std::lock_guard<std::mutex> g(mu);
+      if (!first) first = std::current_exception();
+    }
+  });
+  if (first) std::rethrow_exception(first);
 }
 
 DecoratedSignature decorated(svh_decorated_sig const& s) {
@@ -187,24 +205,14 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
     std::vector<std::vector<Signer>> sgn(ntx);
     // (the C structs -> the mirror's C++ objects, in parallel: a node already
     // holds these objects; the tx set is independent per tx from here on)
-    std::atomic<bool> bad{false};
-    std::string err;
-    std::mutex errMu;
-    hostParallelFor(ntx, 256, [&](size_t a, size_t b) {
-      try {
-        for (size_t t = a; t < b; ++t) {
-          std::memcpy(hashes[t].data(), txs[t].contents_hash, 32);
-          dsigs[t] = sigRange(sigs, txs[t].sig_off, txs[t].nsigs);
-          sgn[t].reserve(txs[t].nsigners);
-          for (uint32_t k = 0; k < txs[t].nsigners; ++k) sgn[t].push_back(signer(signers[txs[t].signer_off + k]));
-        }
-      } catch (std::exception const& e) {
-        std::lock_guard<std::mutex> g(errMu);
-        bad = true;
-        err = e.what();
+    parallelOrThrow(ntx, 256, [&](size_t a, size_t b) {
+      for (size_t t = a; t < b; ++t) {
+        std::memcpy(hashes[t].data(), txs[t].contents_hash, 32);
+        dsigs[t] = sigRange(sigs, txs[t].sig_off, txs[t].nsigs);
+        sgn[t].reserve(txs[t].nsigners);
+        for (uint32_t k = 0; k < txs[t].nsigners; ++k) sgn[t].push_back(signer(signers[txs[t].signer_off + k]));
       }
     });
-    if (bad) throw std::invalid_argument(err);
     pc.lap("txset: marshal");
     SignatureBatchPrefetch pre;
     if (use_prefetch) {
@@ -227,7 +235,7 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
     // With the pre-pass every checker only reads the side table, independent
     // of the others: they run on the host pool.  Without it (the reference's
     // flow: one verifySig per signature) they run in tx order on this thread.
-    if (use_prefetch) hostParallelFor(ntx, 128, check);
+    if (use_prefetch) parallelOrThrow(ntx, 128, check);
     else check(0, ntx);
     pc.lap("txset: checkers");
     return SVH_OK;
@@ -295,7 +303,7 @@ int svh_check_envelopes(const svh_envelope* env, size_t n, const svh_decorated_s
     };
     // (as svh_check_txset: with the pre-pass the checkers only read the side
     // table and the account snapshot, so they run on the host pool)
-    if (prefetch) hostParallelFor(n, 128, check);
+    if (prefetch) parallelOrThrow(n, 128, check);
     else check(0, n);
     return SVH_OK;
   } catch (std::exception const& e) {

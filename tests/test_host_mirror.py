@@ -344,6 +344,23 @@ def test_txset_prefetch_parallel_batch_matches_replay(host, engine, oracle):
     assert pairs > 0 and 0 < want_ok.sum() < len(txs)
 
 
+def test_txset_bad_signer_in_parallel_marshal_is_an_error(host, engine, oracle):
+    """A malformed signer deep inside a set marshalled in parallel parts comes
+    back as SVH_ERR_INVALID_ARG with its message (never an exception escaping a
+    pool thread)."""
+    sign = _oracle_sign_fn(oracle)
+    txs = tg.generate(900, sign, seed=5)
+    T, S, G = tg.to_ctypes(txs)
+    G[len(G) - 3].type = 7  # no such signer type
+    ok = np.zeros(len(txs), np.uint8)
+    used = np.zeros(len(txs), np.uint8)
+    for prefetch in (1, 0):
+        rc = host.svh_check_txset(T, ctypes.c_size_t(len(txs)), S, G, prefetch, ok.ctypes.data_as(ctypes.c_void_p),
+                                  used.ctypes.data_as(ctypes.c_void_p), None)
+        assert rc != 0
+        assert b"signer" in host.svh_last_error_string()
+
+
 @pytest.mark.gpu
 def test_gpu_host_mirror_verify_sig(host, sv, golden):
     if sv.device_count() < 1:
