@@ -114,8 +114,10 @@ typedef int (*svh_keyed_verify_fn)(const uint8_t* pk, const uint8_t* sig, const 
                                    const uint32_t* len, size_t n, uint8_t* verdict, uint8_t* keys);
 void svh_set_test_keyed_verifier(svh_keyed_verify_fn fn);
 void svh_set_keyed_threshold(size_t min_items);
-/* use_prefetch: 0 none; 1 one batch pre-pass into a side table; 2 the same
- * through verifySigBatch (also seeds the verify cache) */
+/* use_prefetch: 0 none; 1 one batch pre-pass into a side table (pairs
+ * enumerated in parallel, each checker finds its tx's pairs by position); 2
+ * the same through verifySigBatch (also seeds the verify cache); 3 as 1 with
+ * the checkers looking their pairs up in the table only */
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs);
 

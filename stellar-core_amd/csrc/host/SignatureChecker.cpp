@@ -332,7 +332,7 @@ bool SignatureBatchPrefetch::lookup(uint256 const& pk, Signature const& sig, Byt
            std::memcmp(&pk_[32 * i], pk.data(), 32) == 0 &&
            (msg.size() == 0 || std::memcmp(&msg_[off_[i]], msg.data(), msg.size()) == 0);
   };
-  if (tx + 1 < txBegin_.size()) {  // the tx's own pairs, contiguous (addBatch)
+  if (tx != kNoTx && tx + 1 < txBegin_.size()) {  // the tx's own pairs, contiguous (addBatch)
     for (size_t i = txBegin_[tx]; i < txBegin_[tx + 1]; ++i)
       if (same(i)) {
         verdict = verdict_[i] != 0;

@@ -227,7 +227,7 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
     auto check = [&](size_t a, size_t b) {
       for (size_t t = a; t < b; ++t) {
         SignatureChecker c(txs[t].protocol, hashes[t], dsigs[t], use_prefetch ? &pre : nullptr,
-                           use_prefetch ? t : SignatureBatchPrefetch::kNoTx);
+                           use_prefetch == 1 || use_prefetch == 2 ? t : SignatureBatchPrefetch::kNoTx);
         ok[t] = c.checkSignature(sgn[t], txs[t].needed_weight) ? 1 : 0;
         all_used[t] = c.checkAllSignaturesUsed() ? 1 : 0;
       }

@@ -342,6 +342,12 @@ def test_txset_prefetch_parallel_batch_matches_replay(host, engine, oracle):
     assert engine.calls - calls_before == 1
     assert (ok1 == want_ok).all() and (used1 == want_used).all()
     assert pairs > 0 and 0 < want_ok.sum() < len(txs)
+    # the same pre-pass, checkers without their tx's position (table lookups only)
+    host.svh_cache_clear()
+    calls_before = engine.calls
+    ok3, used3, pairs3 = _check(host, txs, 3)
+    assert engine.calls - calls_before == 1 and pairs3 == pairs
+    assert (ok3 == want_ok).all() and (used3 == want_used).all()
 
 
 def test_txset_bad_signer_in_parallel_marshal_is_an_error(host, engine, oracle):
@@ -501,6 +507,58 @@ def test_gpu_verify_sig_batch_keyed_matches_hashed(host, sv, golden):
     assert (res[0][0] == d["verdict"][rows]).all()
     assert (res[1][0] == res[0][0]).all()
     assert res[0][1] == res[1][1]
+
+
+@pytest.mark.gpu
+def test_gpu_verify_sig_batch_keyed_large_equals_hashed_cache_state(host, sv, golden):
+    """The large keyed path (threaded walk over key pieces, eviction draws
+    queued while the keys are on their way, misses inserted with their verdict
+    once the engine has returned) against the host-hashed three-phase path on
+    100k items with re-submissions and more than 0xffff distinct keys: equal
+    verdicts, equal hit/miss counts and the same cache contents in the same
+    eviction-vector order."""
+    if sv.device_count() < 1:
+        pytest.skip("no GPU")
+    host.svh_set_test_verifier(None)
+    host.svh_set_test_keyed_verifier(None)
+    d = golden["adversarial"]
+    rng = np.random.default_rng(77)
+    n_rand, n = 90000, 100000
+    # random items (invalid) plus golden rows (valid and invalid), then repeats
+    gold = rng.choice(len(d["verdict"]), n - n_rand, replace=True)
+    pk = np.concatenate([rng.integers(0, 256, (n_rand, 32), dtype=np.uint8), d["pk"][gold]])
+    sig = np.concatenate([rng.integers(0, 256, (n_rand, 64), dtype=np.uint8), d["sig"][gold]])
+    rmsg = rng.integers(0, 256, 32 * n_rand, dtype=np.uint8)
+    msg = np.concatenate([rmsg, d["msg"]])
+    off = np.concatenate([np.arange(n_rand, dtype=np.uint64) * 32, d["msg_off"][gold] + len(rmsg)])
+    ln = np.concatenate([np.full(n_rand, 32, np.uint32), d["msg_len"][gold]])
+    perm = rng.permutation(n)
+    perm[5000::97] = perm[100:100 + len(perm[5000::97])]  # re-submissions of early items
+    pk, sig, off, ln = (np.ascontiguousarray(a[perm]) for a in (pk, sig, off, ln))
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    res = []
+    try:
+        for thr in (0, 256):  # host-hashed, keyed
+            host.svh_set_keyed_threshold(thr)
+            host.svh_cache_clear()
+            host.svh_cache_seed(99)
+            host.svh_cache_counts(None, None)
+            out = np.zeros(n, np.uint8)
+            for a, b in ((0, 30000), (30000, n)):  # two batches: the second walks a full cache
+                rc = host.svh_verify_sig_batch(P(pk[a:b]), P(sig[a:b]), None, P(msg), P(off[a:b]), P(ln[a:b]),
+                                               ctypes.c_size_t(b - a), P(out[a:]))
+                assert rc == 0, host.svh_last_error_string()
+            keys = np.zeros((0x10000, 32), np.uint8)
+            size = host.svh_cache_keys(P(keys), ctypes.c_size_t(0x10000))
+            res.append((out.copy(), _counts(host), keys[:size].copy()))
+    finally:
+        host.svh_set_keyed_threshold(256)
+        host.svh_cache_clear()
+    (o0, c0, k0), (o1, c1, k1) = res
+    assert (o0 == o1).all() and c0 == c1
+    assert len(k0) == 0xFFFF and (k0 == k1).all()
+    gold_rows = perm >= n_rand
+    assert (o1[gold_rows] == d["verdict"][gold[perm[gold_rows] - n_rand]]).all()
 
 
 # ---------------------------------------------------------------- round 2
