@@ -487,7 +487,7 @@ def main():
                 if int(tj.get("batch", -1)) == n and tj.get("kernel_source_sha256") == sv.kernel_source_digest():
                     traffic = tj.get("hbm_bytes_per_launch")
                     prof = {k: tj[k] for k in ("valu_inst_per_verify", "valu_issue_util", "l2_hit_rate",
-                                               "kernel_avg_ns") if k in tj}
+                                               "kernel_avg_ns", "effective_clock_ghz") if k in tj}
                     prof["source"] = "profiles/%s (rocprofv3 PMC, tools/profile_run.sh)" % os.path.basename(tf)
             except Exception:
                 traffic = None
@@ -547,6 +547,11 @@ def main():
                 "frac_vs_survey_nominal_peak": kernel_rate * W_MAD_PER_VERIFY / NOMINAL_PEAK_SURVEY,
                 "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE)",
                 "profiled": prof or None,
+                # the same mads against the peak at the clock the chip holds under
+                # this load (GRBM_GUI_ACTIVE / 8 / wall in the profile; DVFS)
+                "mad_issue_frac_at_profiled_clock": (
+                    kernel_rate * hw_mads / (MAD_LANE_OPS_PER_CLK_CU * cus * prof["effective_clock_ghz"] * 1e9)
+                    if hw_mads and prof.get("effective_clock_ghz") else None),
             },
         }
         if host_api is not None:
