@@ -312,23 +312,25 @@ class RandomEvictionCache {
     while (fcount_ < want) {
       const uint32_t a = (uint32_t)draw_(rng_);
       const uint32_t b = (uint32_t)draw_(rng_);
-      if (fcount_ == future_.size()) {  // grow the ring (unwrapping it)
+      if (fcount_ == future_.size()) {  // grow the ring (unwrapping it; sizes are powers of two)
         std::vector<std::pair<uint32_t, uint32_t>> g(std::max<size_t>(64, 2 * future_.size()));
-        for (size_t k = 0; k < fcount_; ++k) g[k] = future_[(fhead_ + k) % future_.size()];
+        for (size_t k = 0; k < fcount_; ++k) g[k] = futureAt(k);
         future_.swap(g);
         fhead_ = 0;
       }
-      future_[(fhead_ + fcount_) % future_.size()] = {a, b};
+      future_[(fhead_ + fcount_) & (future_.size() - 1)] = {a, b};
       ++fcount_;
     }
   }
-  std::pair<uint32_t, uint32_t> const& futureAt(size_t k) const { return future_[(fhead_ + k) % future_.size()]; }
+  std::pair<uint32_t, uint32_t> const& futureAt(size_t k) const {
+    return future_[(fhead_ + k) & (future_.size() - 1)];
+  }
   void evictOne() {
     const size_t sz = ordId_.size();
     if (sz == 0) return;
     drawAhead(kAhead + 1);
     const size_t ia = futureAt(0).first, ib = futureAt(0).second;
-    fhead_ = (fhead_ + 1) % future_.size();
+    fhead_ = (fhead_ + 1) & (future_.size() - 1);
     --fcount_;
     {  // kAhead ahead: the candidates' order-array entries
       auto const& f = futureAt(kAhead - 1);
@@ -421,6 +423,8 @@ using Item = PubKeyUtils::VerifyItem;
 // keyed batches at least this large walk the cache on the calling thread while
 // the engine call runs on a helper (verifySigBatch)
 constexpr size_t kThreadedWalkMin = 16384;
+// eviction draws queued ahead by a waiting walk at most (8 MB of pairs)
+constexpr size_t kPreDrawMax = size_t(1) << 20;
 
 // Per-thread scratch reused across calls: a large batch does not pay fresh
 // page faults for its index, key and pointer arrays every time.
@@ -694,12 +698,13 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
           continue;
         }
         if (f || done == E) break;
-        if (drawn < E - done) {
+        if (drawn < std::min<size_t>(E - done, kPreDrawMax)) {
           // waiting for keys: queue the eviction draws the walk may need
-          // (at most one per remaining item), a slice per lock hold
+          // (at most one per remaining item, at most kPreDrawMax queued), a
+          // slice per lock hold
           std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
           const size_t before = gVerifySigCache.queuedDraws();
-          drawn = gVerifySigCache.preDraw(E - done);
+          drawn = gVerifySigCache.preDraw(std::min<size_t>(E - done, kPreDrawMax));
           if (drawn == before) drawn = E;  // (nothing more to queue)
           continue;
         }
