@@ -46,3 +46,43 @@ PY
 TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$(gcc -print-file-name=libtsan.so) \
     python3 $O/mb.py $O/libstellar_host.so "$R/tests/native/libhostcore.so" > $O/out_mb.txt 2>&1 || true
 echo "micro-batcher flood: TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out_mb.txt || true); result: $(tail -1 $O/out_mb.txt)"
+# the tx-set pre-pass (round 3): parallel marshal, SignatureBatchPrefetch::addBatch parts and
+# checkers on the pool, with the native stub engine; and the large keyed walk (threaded walk,
+# pre-drawn evictions, inline resolve) with the native keyed stub
+cat > $O/txset.py <<'PY'
+import ctypes, os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(sys.argv[3], "tests"))
+import txset_gen as tg
+host = ctypes.CDLL(sys.argv[1]); stub = ctypes.CDLL(sys.argv[2])
+host.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+host.svh_set_test_keyed_verifier.argtypes = [ctypes.c_void_p]
+host.svh_set_keyed_threshold.argtypes = [ctypes.c_size_t]
+rng = np.random.default_rng(3)
+def sign(reqs):  # random keys and signatures: the stub engine accepts all
+    return [(rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), rng.integers(0, 256, 64, dtype=np.uint8).tobytes())
+            for _ in reqs]
+txs = tg.generate(2000, sign, seed=7)
+T, S, G = tg.to_ctypes(txs)
+host.svh_set_test_verifier(ctypes.cast(stub.hc_stub_verify, ctypes.c_void_p))
+ok = np.zeros(len(txs), np.uint8); used = np.zeros(len(txs), np.uint8)
+for pf in (1, 3, 1):
+    rc = host.svh_check_txset(T, ctypes.c_size_t(len(txs)), S, G, pf, ok.ctypes.data_as(ctypes.c_void_p),
+                              used.ctypes.data_as(ctypes.c_void_p), None)
+    assert rc == 0, rc
+host.svh_set_test_verifier(None)
+host.svh_set_test_keyed_verifier(ctypes.cast(stub.hc_stub_keyed, ctypes.c_void_p))
+host.svh_set_keyed_threshold(1)
+n = 40000
+pk = rng.integers(0, 256, (n, 32), dtype=np.uint8); sig = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+msg = rng.integers(0, 256, 32 * n, dtype=np.uint8)
+off = np.arange(n, dtype=np.uint64) * 32; ln = np.full(n, 32, np.uint32); out = np.zeros(n, np.uint8)
+P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+for _ in range(3):
+    rc = host.svh_verify_sig_batch(P(pk), P(sig), None, P(msg), P(off), P(ln), ctypes.c_size_t(n), P(out))
+    assert rc == 0, rc
+print("ok")
+PY
+TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$(gcc -print-file-name=libtsan.so) \
+    python3 $O/txset.py $O/libstellar_host.so "$R/tests/native/libhostcore.so" "$R" > $O/out_txset.txt 2>&1 || true
+echo "tx-set pre-pass + keyed walk: TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out_txset.txt || true); result: $(tail -1 $O/out_txset.txt)"
