@@ -418,6 +418,7 @@ std::atomic<PubKeyUtils::KeyedBatchVerifyFn> gTestKeyedVerifier{nullptr};
 std::atomic<size_t> gKeyedThreshold{256};
 std::atomic<size_t> gCpuThreshold{1};
 const bool gTrace = getenv("SV_HOST_TRACE") != nullptr;  // stage timings of keyed batches to stderr
+std::chrono::steady_clock::time_point gTraceMarshal;   // (SV_HOST_TRACE: engine inputs marshalled)
 
 using Item = PubKeyUtils::VerifyItem;
 // keyed batches at least this large walk the cache on the calling thread while
@@ -527,13 +528,16 @@ int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, u
   st.sig.resize(n);
   st.msg.resize(n);
   st.len.resize(n);
-  for (size_t i = 0; i < n; ++i) {
+  // (each item's key is a pointer to chase: on the pool for large batches,
+  // this is in front of the first piece of keys)
+  parallelFor(n, 16384, [&](size_t i) {
     Item const& it = items[rows[i]];
     st.pk[i] = it.key->ed25519().data();
     st.sig[i] = it.signature.data();
     st.msg[i] = it.msg.data();
     st.len[i] = (uint32_t)it.msg.size();
-  }
+  });
+  if (gTrace) gTraceMarshal = std::chrono::steady_clock::now();
   if (keysReady)
     return sv_ed25519_verify_batch_gather_progress(st.pk.data(), st.sig.data(), st.msg.data(), st.len.data(), n,
                                                    verdict, kb, runProgress, keysReady, nullptr);
@@ -567,16 +571,41 @@ Hash verifySigCacheKey(PublicKey const& key, ByteSlice const& signature, ByteSli
 }
 
 std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vector<Hash>* keysOut) {
+  const auto tEnter = gTrace ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   const size_t n = items.size();
   std::vector<bool> out(n, false);
   Scratch& sc = scratch();
   std::vector<size_t>& rows = sc.rows;  // eligible items
   rows.clear();
-  for (size_t i = 0; i < n; ++i) {
-    if (items[i].key->type() != PUBLIC_KEY_TYPE_ED25519)
-      throw std::invalid_argument("verifySigBatch: non-ed25519 key");  // releaseAssert, SecretKey.cpp:440
-    if (items[i].signature.size() != 64) continue;                   // SecretKey.cpp:441-444
-    rows.push_back(i);
+  const size_t parts = std::min<size_t>(hostPool().size() + 1, n / 16384);
+  if (parts <= 1) {
+    for (size_t i = 0; i < n; ++i) {
+      if (items[i].key->type() != PUBLIC_KEY_TYPE_ED25519)
+        throw std::invalid_argument("verifySigBatch: non-ed25519 key");  // releaseAssert, SecretKey.cpp:440
+      if (items[i].signature.size() != 64) continue;                   // SecretKey.cpp:441-444
+      rows.push_back(i);
+    }
+  } else {
+    // the same checks and the same rows, on the pool: count per part, then
+    // fill each part's rows at its offset
+    std::vector<size_t> cnt(parts + 1, 0);
+    std::atomic<bool> bad{false};
+    hostPool().run(parts, [&](size_t t) {
+      size_t c = 0;
+      for (size_t i = n * t / parts, b = n * (t + 1) / parts; i < b; ++i) {
+        if (items[i].key->type() != PUBLIC_KEY_TYPE_ED25519) bad.store(true, std::memory_order_relaxed);
+        c += items[i].signature.size() == 64;
+      }
+      cnt[t + 1] = c;
+    });
+    if (bad.load()) throw std::invalid_argument("verifySigBatch: non-ed25519 key");  // releaseAssert, SecretKey.cpp:440
+    for (size_t t = 0; t < parts; ++t) cnt[t + 1] += cnt[t];
+    rows.resize(cnt[parts]);
+    hostPool().run(parts, [&](size_t t) {
+      size_t o = cnt[t];
+      for (size_t i = n * t / parts, b = n * (t + 1) / parts; i < b; ++i)
+        if (items[i].signature.size() == 64) rows[o++] = i;  // SecretKey.cpp:441-444
+    });
   }
   if (keysOut) keysOut->assign(n, Hash{});
   const size_t E = rows.size();
@@ -720,8 +749,10 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
       if (trace) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         const auto tD = std::chrono::steady_clock::now();
-        fprintf(stderr, "[verifySigBatch keyed n=%zu] keys ready %.3f ms, walk %.3f ms, verdicts %.3f ms after walk\n",
-                E, ms(tA, tB), ms(tB, tC), ms(tC, tD));
+        fprintf(stderr,
+                "[verifySigBatch keyed n=%zu] rows %.3f ms, then: inputs marshalled %.3f ms, keys ready %.3f ms, walk "
+                "%.3f ms, verdicts %.3f ms after walk\n",
+                E, ms(tEnter, tA), gTraceMarshal > tA ? ms(tA, gTraceMarshal) : 0.0, ms(tA, tB), ms(tB, tC), ms(tC, tD));
       }
     } else {
       ++gFallbacks;

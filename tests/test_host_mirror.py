@@ -689,6 +689,59 @@ class RefCache:
 
 
 @pytest.mark.parametrize("keyed", [False, True])
+def test_large_batch_rows_with_mixed_signature_sizes(host, hostcore, keyed):
+    """A batch large enough for the pooled eligibility pass (>= 2 x 16384
+    items), with signatures of sizes 0..63 mixed in: the same verdicts, counts
+    and cache contents as the same item stream fed in batches of 1000 (the
+    serial pass).  Items whose signature is not 64 bytes are rejected without
+    touching the cache (SecretKey.cpp:441-444)."""
+    rng = np.random.default_rng(515)
+    n = 50000
+    pk = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    sig = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+    sl = np.full(n, 64, np.uint32)
+    odd = rng.choice(n, 700, replace=False)
+    sl[odd] = rng.choice([0, 1, 32, 63], len(odd))  # (the C-ABI takes n x 64 signature bytes)
+    msg = rng.integers(0, 256, 32 * n, dtype=np.uint8)
+    off = np.arange(n, dtype=np.uint64) * 32
+    ln = np.full(n, 32, np.uint32)
+    h = n // 2  # the second half repeats the first: hits in both feeds
+    pk[h:], sig[h:], off[h:] = pk[:h], sig[:h], off[:h]
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    stub = ctypes.cast(hostcore.hc_stub_keyed if keyed else hostcore.hc_stub_verify, ctypes.c_void_p)
+    res = []
+    try:
+        if keyed:
+            host.svh_set_test_keyed_verifier(stub)
+            host.svh_set_keyed_threshold(1)
+        else:
+            host.svh_set_test_verifier(stub)
+            host.svh_set_keyed_threshold(0)
+        for step in (n, 1000):
+            host.svh_cache_clear()
+            host.svh_cache_seed(5)
+            host.svh_cache_counts(None, None)
+            out = np.zeros(n, np.uint8)
+            for a in range(0, n, step):
+                b = min(n, a + step)
+                rc = host.svh_verify_sig_batch(P(pk[a:]), P(sig[a:]), P(sl[a:]), P(msg), P(off[a:]), P(ln[a:]),
+                                               ctypes.c_size_t(b - a), P(out[a:]))
+                assert rc == 0, host.svh_last_error_string()
+            keys = np.zeros((0x10000, 32), np.uint8)
+            size = host.svh_cache_keys(P(keys), ctypes.c_size_t(0x10000))
+            res.append((out.copy(), _counts(host), keys[:size].copy()))
+    finally:
+        host.svh_set_test_verifier(None)
+        host.svh_set_test_keyed_verifier(None)
+        host.svh_set_keyed_threshold(256)
+        host.svh_cache_clear()
+    (o0, c0, k0), (o1, c1, k1) = res
+    assert (o0 == o1).all() and c0 == c1 and (k0 == k1).all()
+    assert not o0[odd].any() and o0[sl == 64].all()
+    assert sum(c0) == n - len(odd) and c0[0] > 0
+
+
+@pytest.mark.parametrize("keyed", [False, True])
 def test_cache_eviction_matches_sequential_reference(host, hostcore, keyed):
     """Overfill the 0xffff cache through verifySigBatch (3-phase pending
     inserts, or the keyed single walk) and compare the surviving keys, their
