@@ -160,7 +160,7 @@ class RandomEvictionCache {
 
   explicit RandomEvictionCache(size_t maxSize) : maxSize_(maxSize), draw_(0, maxSize) {
     size_t cap = 16;
-    while (cap < 2 * (maxSize + 1)) cap <<= 1;
+    while (cap < 8 * (maxSize + 1)) cap <<= 1;
     table_.assign(cap, 0u);
     mask_ = cap - 1;
     entries_.reserve(maxSize + 1);
@@ -436,6 +436,9 @@ struct Scratch {
   std::vector<uint32_t> ref, ids;
   std::vector<const uint8_t*> pk, sig, msg;
   std::vector<uint32_t> len;
+  // pk / sig / msg / len already hold the engine inputs of `rows` (filled by
+  // verifySigBatch's pooled row pass; gpuVerify then skips its own)
+  bool rowsMarshalled = false;
   // SoA copy for the test hooks (the engine itself gathers)
   std::vector<uint8_t> ppk, psig, pmsg;
   std::vector<uint64_t> poff;
@@ -524,19 +527,22 @@ int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, u
     packForTestHook(items, rows, st);
     return tv(st.ppk.data(), st.psig.data(), st.pmsg.data(), st.poff.data(), st.plen.data(), n, verdict);
   }
-  st.pk.resize(n);
-  st.sig.resize(n);
-  st.msg.resize(n);
-  st.len.resize(n);
-  // (each item's key is a pointer to chase: on the pool for large batches,
-  // this is in front of the first piece of keys)
-  parallelFor(n, 16384, [&](size_t i) {
-    Item const& it = items[rows[i]];
-    st.pk[i] = it.key->ed25519().data();
-    st.sig[i] = it.signature.data();
-    st.msg[i] = it.msg.data();
-    st.len[i] = (uint32_t)it.msg.size();
-  });
+  if (!(st.rowsMarshalled && &rows == &st.rows && st.pk.size() == n)) {
+    st.pk.resize(n);
+    st.sig.resize(n);
+    st.msg.resize(n);
+    st.len.resize(n);
+    // (each item's key is a pointer to chase: on the pool for large batches,
+    // this is in front of the first piece of keys)
+    parallelFor(n, 16384, [&](size_t i) {
+      Item const& it = items[rows[i]];
+      st.pk[i] = it.key->ed25519().data();
+      st.sig[i] = it.signature.data();
+      st.msg[i] = it.msg.data();
+      st.len[i] = (uint32_t)it.msg.size();
+    });
+  }
+  st.rowsMarshalled = false;
   if (gTrace) gTraceMarshal = std::chrono::steady_clock::now();
   if (keysReady)
     return sv_ed25519_verify_batch_gather_progress(st.pk.data(), st.sig.data(), st.msg.data(), st.len.data(), n,
@@ -577,6 +583,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
   Scratch& sc = scratch();
   std::vector<size_t>& rows = sc.rows;  // eligible items
   rows.clear();
+  sc.rowsMarshalled = false;
   const size_t parts = std::min<size_t>(hostPool().size() + 1, n / 16384);
   if (parts <= 1) {
     for (size_t i = 0; i < n; ++i) {
@@ -600,12 +607,28 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     });
     if (bad.load()) throw std::invalid_argument("verifySigBatch: non-ed25519 key");  // releaseAssert, SecretKey.cpp:440
     for (size_t t = 0; t < parts; ++t) cnt[t + 1] += cnt[t];
-    rows.resize(cnt[parts]);
+    const size_t E = cnt[parts];
+    rows.resize(E);
+    // (the engine's input pointers in the same pass: gpuVerify of these rows
+    // need not walk the items again)
+    sc.pk.resize(E);
+    sc.sig.resize(E);
+    sc.msg.resize(E);
+    sc.len.resize(E);
     hostPool().run(parts, [&](size_t t) {
       size_t o = cnt[t];
-      for (size_t i = n * t / parts, b = n * (t + 1) / parts; i < b; ++i)
-        if (items[i].signature.size() == 64) rows[o++] = i;  // SecretKey.cpp:441-444
+      for (size_t i = n * t / parts, b = n * (t + 1) / parts; i < b; ++i) {
+        Item const& it = items[i];
+        if (it.signature.size() != 64) continue;  // SecretKey.cpp:441-444
+        rows[o] = i;
+        sc.pk[o] = it.key->ed25519().data();
+        sc.sig[o] = it.signature.data();
+        sc.msg[o] = it.msg.data();
+        sc.len[o] = (uint32_t)it.msg.size();
+        ++o;
+      }
     });
+    sc.rowsMarshalled = true;
   }
   if (keysOut) keysOut->assign(n, Hash{});
   const size_t E = rows.size();

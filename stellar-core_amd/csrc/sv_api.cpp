@@ -645,19 +645,22 @@ Image image_of(const HostIn& in, size_t lo, size_t m, size_t* msg_total) {
 
 // Packing [lo, lo + m) into h (layout `im`): the message offsets first, then
 // rows [r0, r1) of the chunk, in parallel for large ranges.
-void pack_offsets(const HostIn& in, size_t lo, size_t m, const Image& im, uint8_t* h) {
+// (rows [r0, r1), the first at message offset pos; returns the offset past r1)
+uint64_t pack_offsets(const HostIn& in, size_t lo, size_t r0, size_t r1, uint64_t pos, const Image& im, uint8_t* h) {
   uint64_t* offs = (uint64_t*)(h + im.o_off);
   if (im.var) {
-    uint64_t pos = 0;
-    for (size_t i = 0; i < m; ++i) {
+    for (size_t i = r0; i < r1; ++i) {
       offs[i] = pos;
       pos += in.len[lo + i];
     }
   }
+  return pos;
 }
-void pack_rows(const HostIn& in, size_t lo, size_t r0, size_t r1, const Image& im, uint8_t* h) {
+// kPart: bytes per helper task (a keyed batch's pieces take smaller ones:
+// the first verify launch waits for the last piece)
+void pack_rows(const HostIn& in, size_t lo, size_t r0, size_t r1, const Image& im, uint8_t* h,
+               size_t kPart = 1u << 20) {
   const uint64_t* offs = (const uint64_t*)(h + im.o_off);
-  const size_t kPart = 1u << 20;  // bytes per helper task
   const size_t m = r1 - r0;
   const size_t est = im.bytes / std::max<size_t>(1, (im.o_sig / 32)) * m;  // (bytes of these rows, roughly)
   const size_t parts = std::max<size_t>(1, std::min<size_t>(pool().size() + 1, est / kPart));
@@ -691,7 +694,7 @@ void pack_rows(const HostIn& in, size_t lo, size_t r0, size_t r1, const Image& i
   });
 }
 void pack(const HostIn& in, size_t lo, size_t m, const Image& im, uint8_t* h) {
-  pack_offsets(in, lo, m, im, h);
+  pack_offsets(in, lo, 0, m, 0, im, h);
   pack_rows(in, lo, 0, m, im, h);
 }
 // H2D of rows [a, b) of a packed image (each section's slice); msg_total: the
@@ -745,10 +748,21 @@ struct KeysCb {
   void operator()(size_t ready) const { fn(ctx, ready); }
 };
 // A one-chunk keyed batch of at least kKeyPieceMin rows sends its keys up in
-// pieces of about kKeyPieceRows (at most kKeyPiecesMax pieces): the caller's
-// cache walk starts on the first piece while later ones are packed, copied
-// and hashed (the walk, ~30 ns per row, is the slower side).
-constexpr size_t kKeyPieceRows = 8192, kKeyPieceMin = 8192, kKeyPiecesMax = 16;
+// pieces (key_pieces): the caller's cache walk starts on the first piece while
+// later ones are packed, copied and hashed.  The first piece is kKeyPieceFirst
+// rows, so the walk starts as early as it can; each later piece is twice the
+// one before, at most kKeyPieceMax rows (a piece costs ~10 HIP calls on this
+// thread: fewer pieces bring the last one, and the verify launch behind it,
+// forward).
+constexpr size_t kKeyPieceMin = 8192, kKeyPieceFirst = 2048, kKeyPieceMax = 1 << 15;
+// Row bounds of the pieces of an m-row batch: b[0] = 0 < b[1] < ... < b[P] = m.
+std::vector<size_t> key_pieces(size_t m) {
+  if (m < kKeyPieceMin) return {0, m};
+  std::vector<size_t> b{0};
+  for (size_t len = kKeyPieceFirst; b.back() < m; len = std::min(2 * len, kKeyPieceMax))
+    b.push_back(m - b.back() < len + len / 2 ? m : b.back() + len);  // (no runt last piece)
+  return b;
+}
 
 // Runs fn(0), fn(1), ... fn(P - 1) on a thread of its own, fn(k) once piece
 // k's events have been recorded (recorded(k + 1)); join() returns the first
@@ -832,11 +846,17 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
   const size_t chunk = std::min(n, stage_chunk());
   int rc;
   const int ktm = kt_mode();
-  const bool tables = verdict && resolve_path(path, chunk) != SV_PATH_LATENCY &&
-                      (ktm == 1 || (ktm == 2 && repeated_keys(in, n)));
+  // (decided at the first launch: a keyed batch's first pieces go up before it)
+  int tables = -1;
+  auto trace_at = [](const char* what) {
+    if (stage_trace())
+      fprintf(stderr, "SV_STAGE_TRACE %s at %.1f us\n", what,
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - g_trace_t0).count());
+  };
   // the largest launch first, so the workspace never grows under a running kernel
   if (verdict && (rc = ensure_ws(D, sv_verify_ws_bytes(resolve_path(path, chunk), grid_for(D, chunk), chunk))))
     return rc;
+  trace_at("workspace");
   const size_t out_per = (verdict ? 1 : 0) + (keys ? 32 : 0);
   // one chunk (latency-bound batches): everything on the kernel stream, no
   // cross-stream event waits
@@ -872,14 +892,15 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     const bool early = single && kcb && keys && verdict;
     // a one-chunk keyed batch with a keys-ready callback: pack, copy up, hash
     // and copy the keys down in pieces, so the caller's walk starts early
-    const size_t P =
-        early && m >= kKeyPieceMin ? std::min(kKeyPiecesMax, std::max<size_t>(2, (m + kKeyPieceRows - 1) / kKeyPieceRows)) : 1;
+    const std::vector<size_t> pb = early ? key_pieces(m) : std::vector<size_t>{0, m};
+    const size_t P = pb.size() - 1;
     while (s.pev.size() < P) {
       hipEvent_t e;
       SV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       s.pev.push_back(e);
     }
     const auto t_pack = stage_trace() ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+    trace_at("staging");
     if (P == 1) {
       pack(in, lo, m, im, hp);
       SV_HIP(hipMemcpyAsync(s.d_in.p, s.h_in.p, im.bytes, hipMemcpyHostToDevice, up_s));
@@ -903,8 +924,10 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
       // one thread, in order).
       const auto t0 = g_trace_t0;
       auto us = [t0] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(); };
-      notifier.start(D.phys, P, [&, m, lo](size_t k) -> int {
-        const size_t a = m * k / P, b = m * (k + 1) / P;
+      // (pb and us by value: an error return leaves this scope before the
+      // notifier is joined)
+      notifier.start(D.phys, P, [&, m, lo, pb, us](size_t k) -> int {
+        const size_t a = pb[k], b = pb[k + 1];
         SV_HIP(hipEventSynchronize(s.pev[k]));
         if (stage_trace()) fprintf(stderr, "SV_STAGE_TRACE keys piece %zu down at %.1f us\n", k, us());
         std::memcpy(keys + 32 * (lo + a), (uint8_t*)s.h_out.p + m + 32 * a, 32 * (b - a));
@@ -912,12 +935,19 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
         if (stage_trace()) fprintf(stderr, "SV_STAGE_TRACE keys piece %zu walked at %.1f us\n", k, us());
         return SV_OK;
       });
-      pack_offsets(in, lo, m, im, hp);
-      if (stage_trace()) fprintf(stderr, "SV_STAGE_TRACE offsets at %.1f us\n", us());
+      uint64_t pos = 0;  // (each piece writes its own message offsets first)
       for (size_t k = 0; k < P; ++k) {
-        const size_t a = m * k / P, b = m * (k + 1) / P;
-        pack_rows(in, lo, a, b, im, hp);
-        if ((rc = upload_rows(im, m, a, b, in.fixed, msg_total, hp, d, D.stream))) return rc;
+        const size_t a = pb[k], b = pb[k + 1];
+        pos = pack_offsets(in, lo, a, b, pos, im, hp);
+        if (im.var && b < m) ((uint64_t*)(hp + im.o_off))[b] = pos;  // (upload_rows reads the piece's end there)
+        pack_rows(in, lo, a, b, im, hp, 1u << 16);
+        if (k == 0) trace_at("piece 0 packed");
+        // uploads on the copy stream: piece k + 1 goes up while piece k hashes
+        // (the slot's earlier work is complete: drained above)
+        if ((rc = upload_rows(im, m, a, b, in.fixed, msg_total, hp, d, D.h2d))) return rc;
+        SV_HIP(hipEventRecord(s.up, D.h2d));
+        SV_HIP(hipStreamWaitEvent(D.stream, s.up, 0));
+        if (k == 0) trace_at("piece 0 uploading");
         SV_HIP(sv_launch_hash(0, D.grid * 2, d + 32 * a, d + im.o_sig + 64 * a,
                               d + im.o_msg + (im.var ? 0 : a * (size_t)in.fixed), d_off ? d_off + a : nullptr,
                               d_len ? d_len + a : nullptr, in.fixed, b - a, (uint8_t*)s.d_keys.p + 32 * a, D.stream));
@@ -933,8 +963,10 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     if (stage_trace()) g_trace_pack_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_pack).count();
     if (verdict) {
       const int mode = im.var ? 1 : (in.fixed == 32 ? 0 : 2);
+      if (tables < 0)
+        tables = resolve_path(path, chunk) != SV_PATH_LATENCY && (ktm == 1 || (ktm == 2 && repeated_keys(in, n)));
       if ((rc = launch_locked(D, mode, path, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m,
-                              s.d_verdict.p, nullptr, tables)))
+                              s.d_verdict.p, nullptr, tables != 0)))
         return rc;
     }
     if (!single) {
