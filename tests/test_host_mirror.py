@@ -688,8 +688,8 @@ class RefCache:
             self.ptrs.pop()
 
 
-@pytest.mark.parametrize("keyed", [False, True])
-def test_large_batch_rows_with_mixed_signature_sizes(host, hostcore, keyed):
+@pytest.mark.parametrize("keyed,n_odd", [(False, 700), (True, 700), (True, 0)])
+def test_large_batch_rows_with_mixed_signature_sizes(host, hostcore, keyed, n_odd):
     """A batch large enough for the pooled eligibility pass (>= 2 x 16384
     items), with signatures of sizes 0..63 mixed in: the same verdicts, counts
     and cache contents as the same item stream fed in batches of 1000 (the
@@ -700,7 +700,7 @@ def test_large_batch_rows_with_mixed_signature_sizes(host, hostcore, keyed):
     pk = rng.integers(0, 256, (n, 32), dtype=np.uint8)
     sig = rng.integers(0, 256, (n, 64), dtype=np.uint8)
     sl = np.full(n, 64, np.uint32)
-    odd = rng.choice(n, 700, replace=False)
+    odd = rng.choice(n, n_odd, replace=False)  # (0: every row eligible, the one-pass case)
     sl[odd] = rng.choice([0, 1, 32, 63], len(odd))  # (the C-ABI takes n x 64 signature bytes)
     msg = rng.integers(0, 256, 32 * n, dtype=np.uint8)
     off = np.arange(n, dtype=np.uint64) * 32
