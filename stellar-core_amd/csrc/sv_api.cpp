@@ -42,6 +42,7 @@
 #include <functional>
 #include <mutex>
 #include <random>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -86,6 +87,7 @@ hipError_t sv_launch_comb(int mode, int spw, const void* pk, const void* sig, co
 namespace {
 
 thread_local std::string t_err;
+bool test_knobs_enabled();
 
 int fail(int code, const std::string& msg) {
   t_err = msg;
@@ -381,6 +383,20 @@ int init_locked() {
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
   g_inited = true;
+  // SV_TEST_STUB_SLOTS=k (with SV_TEST_KNOBS=1, no GPU): k slots on no device,
+  // so the slot table's lifetime can be stressed on a CPU-only host (every
+  // call that reaches a slot's resources fails with SV_ERR_HIP)
+  const size_t stub = (e != hipSuccess || n <= 0) && test_knobs_enabled() ? env_size("SV_TEST_STUB_SLOTS", 0) : 0;
+  if (stub) {
+    const size_t k = g_map.empty() ? stub : g_map.size();
+    for (size_t i = 0; i < k; ++i) {
+      Device* D = new Device();
+      D->slot = (int)i;
+      D->phys = -1;
+      g_devs.push_back(D);
+    }
+    return SV_OK;
+  }
   if (e != hipSuccess || n <= 0) return fail(SV_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
   std::vector<int> map = g_map;
   if (map.empty()) {
@@ -1549,6 +1565,27 @@ void shutdown_locked() {
   g_inited = false;
 }
 
+// Lifetime of the slot table.  Every entry point that reaches a Device holds
+// g_life shared for the whole call (LifeGuard); sv_shutdown and
+// sv_set_device_map take it exclusively, so no Device is deleted while a call
+// (or the helper-pool work it fans out) still uses it.  The reference's cache
+// controls are likewise safe against concurrent verifySig (SecretKey.cpp
+// :317-330, one mutex).  A thread takes it once however deep its entry points
+// nest: re-acquiring a shared lock behind a queued writer would deadlock.
+// Lock order: g_life, then g_mu, then a slot's lat.mu, then its mu.
+std::shared_mutex g_life;
+thread_local int t_life_depth = 0;
+struct LifeGuard {
+  LifeGuard() {
+    if (t_life_depth++ == 0) g_life.lock_shared();
+  }
+  ~LifeGuard() {
+    if (--t_life_depth == 0) g_life.unlock_shared();
+  }
+  LifeGuard(const LifeGuard&) = delete;
+  LifeGuard& operator=(const LifeGuard&) = delete;
+};
+
 Device* device_arg(int device) {
   if (device < 0 || device >= (int)g_devs.size()) return nullptr;
   return g_devs[device];
@@ -1561,14 +1598,19 @@ extern "C" {
 int sv_init(void) { return ensure_init(); }
 
 void sv_shutdown(void) {
+  if (t_life_depth != 0) return;  // (from inside an engine call, e.g. a keys-ready callback: refused)
+  std::unique_lock<std::shared_mutex> life(g_life);  // waits for every in-flight call
   std::lock_guard<std::mutex> g(g_mu);
   shutdown_locked();
 }
 
 int sv_set_device_map(const int* physical, int count) {
   if (count < 0 || (count > 0 && !physical)) return fail(SV_ERR_INVALID_ARG, "bad device map");
+  if (t_life_depth != 0) return fail(SV_ERR_INVALID_ARG, "sv_set_device_map called from inside an engine call");
   // teardown and the new map in ONE critical section: a concurrent first use
-  // cannot re-initialise with the old map in between
+  // cannot re-initialise with the old map in between; in-flight calls finish
+  // first (g_life)
+  std::unique_lock<std::shared_mutex> life(g_life);
   std::lock_guard<std::mutex> g(g_mu);
   shutdown_locked();
   g_map.assign(physical, physical + count);
@@ -1583,6 +1625,7 @@ int sv_set_device_map(const int* physical, int count) {
 }
 
 int sv_device_count(void) {
+  LifeGuard life_;
   int rc = ensure_init();
   if (rc) return rc;
   return (int)g_devs.size();
@@ -1596,6 +1639,7 @@ const char* sv_version(void) {
 
 int sv_ed25519_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                             const uint32_t* msg_len, size_t n, uint8_t* verdict, const sv_opts* opts) {
+  LifeGuard life_;
   HostIn in;
   in.pk = pk;
   in.sig = sig;
@@ -1607,6 +1651,7 @@ int sv_ed25519_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t
 
 int sv_ed25519_verify_batch_fixed(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_len,
                                   size_t n, uint8_t* verdict, const sv_opts* opts) {
+  LifeGuard life_;
   if (msg_len == 0) {
     // zero-length messages: route through the variable-length path
     std::vector<uint64_t> off(n, 0);
@@ -1625,6 +1670,7 @@ int sv_ed25519_verify_batch_fixed(const uint8_t* pk, const uint8_t* sig, const u
 int sv_ed25519_verify_batch_gather(const uint8_t* const* pk, const uint8_t* const* sig, const uint8_t* const* msg,
                                    const uint32_t* msg_len, size_t n, uint8_t* verdict, uint8_t* keys,
                                    const sv_opts* opts) {
+  LifeGuard life_;
   if (n && (!pk || !verdict)) return fail(SV_ERR_INVALID_ARG, "null buffer");
   HostIn in;
   in.ppk = pk;
@@ -1637,6 +1683,7 @@ int sv_ed25519_verify_batch_gather(const uint8_t* const* pk, const uint8_t* cons
 int sv_ed25519_verify_batch_gather_cb(const uint8_t* const* pk, const uint8_t* const* sig,
                                       const uint8_t* const* msg, const uint32_t* msg_len, size_t n, uint8_t* verdict,
                                       uint8_t* keys, void (*keys_ready)(void* ctx), void* ctx, const sv_opts* opts) {
+  LifeGuard life_;
   if (n && (!pk || !verdict || !keys || !keys_ready)) return fail(SV_ERR_INVALID_ARG, "null buffer");
   HostIn in;
   in.ppk = pk;
@@ -1662,6 +1709,7 @@ int sv_ed25519_verify_batch_gather_progress(const uint8_t* const* pk, const uint
                                             uint8_t* verdict, uint8_t* keys,
                                             void (*keys_ready)(void* ctx, size_t ready), void* ctx,
                                             const sv_opts* opts) {
+  LifeGuard life_;
   if (n && (!pk || !verdict || !keys || !keys_ready)) return fail(SV_ERR_INVALID_ARG, "null buffer");
   HostIn in;
   in.ppk = pk;
@@ -1677,6 +1725,7 @@ int sv_ed25519_verify_batch_gather_progress(const uint8_t* const* pk, const uint
 int sv_ed25519_verify_batch_keyed(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                                   const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* verdict,
                                   uint8_t* keys, const sv_opts* opts) {
+  LifeGuard life_;
   if (!verdict || !keys) return n ? fail(SV_ERR_INVALID_ARG, "null verdict/keys") : SV_OK;
   HostIn in;
   in.pk = pk;
@@ -1689,6 +1738,7 @@ int sv_ed25519_verify_batch_keyed(const uint8_t* pk, const uint8_t* sig, const u
 
 int sv_verify_cache_keys(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                          const uint32_t* msg_len, size_t n, uint8_t* keys, const sv_opts* opts) {
+  LifeGuard life_;
   if (!keys) return n ? fail(SV_ERR_INVALID_ARG, "null keys") : SV_OK;
   HostIn in;
   in.pk = pk;
@@ -1701,6 +1751,7 @@ int sv_verify_cache_keys(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
 
 int sv_sha256_batch(const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n, uint8_t* digests,
                     const sv_opts* opts) {
+  LifeGuard life_;
   if (n == 0) return check_opts(opts);
   if (!digests) return fail(SV_ERR_INVALID_ARG, "null digests");
   HostIn in;
@@ -1750,17 +1801,20 @@ static int hash_device(int kind, int device, const void* d_pk, const void* d_sig
 int sv_verify_cache_keys_device(int device, const void* d_pk, const void* d_sig, const void* d_msg,
                                 const uint64_t* d_msg_off, const uint32_t* d_msg_len, uint32_t fixed_msg_len,
                                 size_t n, void* d_keys, void* stream) {
+  LifeGuard life_;
   return hash_device(0, device, d_pk, d_sig, d_msg, d_msg_off, d_msg_len, fixed_msg_len, n, d_keys, stream);
 }
 
 int sv_sha256_device(int device, const void* d_data, const uint64_t* d_off, const uint32_t* d_len,
                      uint32_t fixed_len, size_t n, void* d_digests, void* stream) {
+  LifeGuard life_;
   return hash_device(1, device, nullptr, nullptr, d_data, d_off, d_len, fixed_len, n, d_digests, stream);
 }
 
 int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, const void* d_msg,
                              const uint64_t* d_msg_off, const uint32_t* d_msg_len, uint32_t fixed_msg_len,
                              size_t n, void* d_verdict, void* d_bitmap, void* stream) {
+  LifeGuard life_;
   int rc = ensure_init();
   if (rc) return rc;
   Device* Dp = device_arg(device);
@@ -1813,11 +1867,13 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
 }
 
 int sv_set_kernel_path(int path) {
+  LifeGuard life_;
   if (path != SV_PATH_AUTO && path != SV_PATH_THROUGHPUT && path != SV_PATH_LATENCY) return SV_ERR_INVALID_ARG;
   return g_path.exchange(path);
 }
 
 int sv_set_debug_flags(uint32_t flags) {
+  LifeGuard life_;
   if (flags & ~(SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_FAIL | SV_DBG_PREP_ONLY | SV_DBG_KEY_COLLIDE))
     return SV_ERR_INVALID_ARG;
   // the knobs that change what a call returns (FAIL: every call errs;
@@ -1828,12 +1884,14 @@ int sv_set_debug_flags(uint32_t flags) {
 }
 
 int sv_set_min_shard(size_t n) {
+  LifeGuard life_;
   g_min_shard.store(n);
   return SV_OK;
 }
 
 int sv_ed25519_sign_device(int device, const void* d_seed, const void* d_msg32, size_t n, void* d_pk, void* d_sig,
                            void* stream) {
+  LifeGuard life_;
   int rc = ensure_init();
   if (rc) return rc;
   Device* Dp = device_arg(device);
@@ -1858,11 +1916,13 @@ int sv_ed25519_sign_device(int device, const void* d_seed, const void* d_msg32, 
 }
 
 int sv_timing_enable(int enable) {
+  LifeGuard life_;
   g_timing.store(enable ? 1 : 0);
   return SV_OK;
 }
 
 int sv_kernel_time(int device, double* total_ms, uint64_t* launches, uint64_t* signatures) {
+  LifeGuard life_;
   int rc = ensure_init();
   if (rc) return rc;
   Device* Dp = device_arg(device);
@@ -1887,6 +1947,7 @@ int sv_kernel_time(int device, double* total_ms, uint64_t* launches, uint64_t* s
 }
 
 int sv_kernel_time_reset(void) {
+  LifeGuard life_;
   int rc = ensure_init();
   if (rc) return rc;
   for (Device* D : g_devs) {
@@ -1904,6 +1965,7 @@ int sv_kernel_time_reset(void) {
 }
 
 int sv_device_synchronize(int device) {
+  LifeGuard life_;
   int rc = ensure_init();
   if (rc) return rc;
   Device* Dp = device_arg(device);
@@ -1919,12 +1981,14 @@ int sv_device_synchronize(int device) {
 }
 
 int sv_set_key_tables(int mode, size_t slots) {
+  LifeGuard life_;
   if (mode < -1 || mode > 2) return fail(SV_ERR_INVALID_ARG, "key-table mode must be -1, 0, 1 or 2");
   g_kt_slots.store(slots);
   return g_kt_mode.exchange(mode);
 }
 
 int sv_set_key_cache(size_t capacity) {
+  LifeGuard life_;
   if (capacity > ((size_t)1 << 20)) return fail(SV_ERR_INVALID_ARG, "key cache capacity above 2^20 keys");
   std::lock_guard<std::mutex> g0(g_mu);
   g_key_cap.store(capacity);
@@ -1938,6 +2002,7 @@ int sv_set_key_cache(size_t capacity) {
 }
 
 int sv_key_cache_wait(int device) {
+  LifeGuard life_;
   int rc = ensure_init();
   if (rc) return rc;
   Device* Dp = device_arg(device);
@@ -1952,6 +2017,7 @@ int sv_key_cache_wait(int device) {
 }
 
 int sv_key_cache_get_stats(int device, sv_key_cache_stats* out) {
+  LifeGuard life_;
   int rc = ensure_init();
   if (rc) return rc;
   Device* Dp = device_arg(device);
@@ -1982,6 +2048,7 @@ int sv_key_cache_get_stats(int device, sv_key_cache_stats* out) {
 }
 
 int sv_workspace_bytes(int device, size_t* bytes) {
+  LifeGuard life_;
   int rc = ensure_init();
   if (rc) return rc;
   Device* Dp = device_arg(device);
@@ -1992,6 +2059,7 @@ int sv_workspace_bytes(int device, size_t* bytes) {
 }
 
 int sv_pinned_bytes(int device, size_t* bytes) {
+  LifeGuard life_;
   int rc = ensure_init();
   if (rc) return rc;
   Device* Dp = device_arg(device);

@@ -201,7 +201,11 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   if (li - lane >= c.cnt) return;                                        // (wave-uniform)
   const bool active = li < c.cnt;
   const uint64_t ii = c.start + (active ? li : c.cnt - 1);  // idle tail lanes redo the last item
+#ifdef SV_DIAG_PREP_ALIAS  // (diagnostic builds only: table writes into a small region)
+  sv_u4* tabA = p.ws + (li & (uint64_t)(SV_DIAG_PREP_ALIAS - 1)) * SV_SLOT_QUADS_L;
+#else
   sv_u4* tabA = p.ws + li * SV_SLOT_QUADS_L;
+#endif
   sv_u4* tabR = tabA + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
 #ifdef SV_PHASE_PROF
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
@@ -420,7 +424,11 @@ __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cpa
   for (uint64_t base = gtid - lane; base < c.cnt; base += stride) {
     const uint64_t li = base + lane;  // (slots exist up to the chunk's last full wave)
     const bool active = li < c.cnt;
+#ifdef SV_DIAG_TAB_ALIAS  // (diagnostic builds only: wrong verdicts; table reads from a small region)
+    const sv_u4* slot = p.ws + (li & (uint64_t)(SV_DIAG_TAB_ALIAS - 1)) * SV_SLOT_QUADS_L;
+#else
     const sv_u4* slot = p.ws + li * SV_SLOT_QUADS_L;
+#endif
     const sv_u4* tabR = slot + SV_ATAB_ENTRIES * SV_LTAB_QUADS;
     const uint32_t* rw = (const uint32_t*)(c.rec + li * SV_REC_QUADS);
     const uint32_t flags = rw[16 + 2 * SV_LB_DIGITS];

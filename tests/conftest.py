@@ -73,7 +73,7 @@ def load_golden(name):
 
 @pytest.fixture(scope="session")
 def golden():
-    return {n: load_golden(n) for n in ("intree", "valid", "msglen", "adversarial", "lattice_edge")}
+    return {n: load_golden(n) for n in ("intree", "valid", "msglen", "longmsg", "adversarial", "lattice_edge")}
 
 
 def oracle_verdicts(oracle, d, rows=None):

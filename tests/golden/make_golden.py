@@ -16,6 +16,11 @@ Fixture files (numpy .npz, allow_pickle=False):
                  msg_i = SHA-256("SVMSG"||u64le i)  
   msglen.npz     message lengths 0..512 (1- to 5-block SHA-512 paths, incl. the
                  128-384 B SCP statement range of config 4)
+  longmsg.npz    messages of 513 B .. 64 KiB - 1 (survey responses carry an
+                 EncryptedBody up to 64000 B, SurveyManager.cpp:388-393; large
+                 SCP nominations, HerderImpl.cpp:2414-2432): valid rows, a byte
+                 flipped in the first / last block, and signature mutations
+                 (S + L, a flipped R or S bit, another key) over the same bytes
   adversarial.npz  mutation classes: bit flips in R/S/A/msg,
                  S+L / S+2L / S=L, small-order R and A (+/- bit 255),
                  non-canonical y>=p encodings, off-curve A, mixed-order
@@ -151,7 +156,9 @@ class Rows:
         self.cls.append(cid)
         self.expect.append(expect)
 
-    def save(self, name):
+    def save(self, name, share=False):
+        """share: rows with identical message bytes point at one copy (msg_off),
+        so signature-mutation rows over a long message cost no extra bytes."""
         n = len(self.pk)
         verdict = np.array([sod_verify(s, m, p) for p, s, m in zip(self.pk, self.sig, self.msg)], np.uint8)
         orc = np.array([orc_verify(s, m, p) for p, s, m in zip(self.pk, self.sig, self.msg)], np.uint8)
@@ -161,12 +168,23 @@ class Rows:
         assert (exp[has] == verdict[has]).all(), "libsodium disagrees with the reference's expected verdicts"
         lens = np.array([len(m) for m in self.msg], np.uint32)
         off = np.zeros(n, np.uint64)
-        off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        if share:
+            at, parts, pos = {}, [], 0
+            for i, m in enumerate(self.msg):
+                if m not in at:
+                    at[m] = pos
+                    parts.append(m)
+                    pos += len(m)
+                off[i] = at[m]
+            blob = b"".join(parts)
+        else:
+            off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+            blob = b"".join(self.msg)
         np.savez_compressed(
             os.path.join(HERE, name),
             pk=np.frombuffer(b"".join(self.pk), np.uint8).reshape(n, 32),
             sig=np.frombuffer(b"".join(self.sig), np.uint8).reshape(n, 64),
-            msg=np.frombuffer(b"".join(self.msg) or b"", np.uint8),
+            msg=np.frombuffer(blob or b"", np.uint8),
             msg_off=off, msg_len=lens, verdict=verdict,
             cls=np.array(self.cls, np.uint16), expect=exp,
             class_names=np.array(sorted(self.classes, key=self.classes.get)),
@@ -219,6 +237,37 @@ def msglen():
             mm[ln // 2] ^= 0x40
             rows.add("msglen_flip", pk, s, bytes(mm), 0)
     rows.save("msglen.npz")
+
+
+LONG_LENS = (513, 575, 576, 639, 640, 767, 768, 1023, 1024, 1025, 2047, 2048, 4095, 4096, 8191, 16384, 32768,
+             65535)
+
+
+def longmsg():
+    """Messages past 512 B: every length is a valid libsodium signature, the
+    same message with one byte flipped in its first and in its last SHA-512
+    block (R||A||M: the first block holds M[0..63]), and over the valid bytes
+    S + L, one flipped bit of R and of S, and a different signer's key."""
+    rows = Rows()
+    for k, ln in enumerate(LONG_LENS):
+        pk, sk = sod_keypair(seed_of(4_000_000 + k))
+        m = hashlib.shake_256(b"LONG" + struct.pack("<Q", ln)).digest(ln)
+        s = sod_sign(m, sk)
+        rows.add("long_valid", pk, s, m, 1)
+        mm = bytearray(m); mm[ln - 1] ^= 0x01
+        rows.add("long_flip_last", pk, s, bytes(mm), 0)
+        if ln <= 4096:
+            mm = bytearray(m); mm[0] ^= 0x80
+            rows.add("long_flip_first", pk, s, bytes(mm), 0)
+        S = int.from_bytes(s[32:], "little")
+        rows.add("long_S_plus_L", pk, s[:32] + (S + L).to_bytes(32, "little"), m, 0)
+        sb = bytearray(s); sb[7] ^= 0x10
+        rows.add("long_flip_R", pk, bytes(sb), m, 0)
+        sb = bytearray(s); sb[40] ^= 0x02
+        rows.add("long_flip_S", pk, bytes(sb), m, 0)
+        pk2, _ = sod_keypair(seed_of(4_100_000 + k))
+        rows.add("long_other_key", pk2, s, m, 0)
+    rows.save("longmsg.npz", share=True)
 
 
 BLACKLIST = [
@@ -367,9 +416,10 @@ def dataset_digests():
 
 if __name__ == "__main__":
     print("libsodium", SODIUM_VERSION)
-    which = sys.argv[1:] or ["intree", "valid", "msglen", "adversarial", "digests"]
+    which = sys.argv[1:] or ["intree", "valid", "msglen", "longmsg", "adversarial", "digests"]
     if "intree" in which: intree()
     if "valid" in which: valid()
     if "msglen" in which: msglen()
+    if "longmsg" in which: longmsg()
     if "adversarial" in which: adversarial()
     if "digests" in which: dataset_digests()

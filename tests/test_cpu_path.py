@@ -13,7 +13,7 @@ import pytest
 from conftest import oracle_verdicts
 
 
-@pytest.mark.parametrize("name", ["intree", "valid", "msglen", "adversarial", "lattice_edge"])
+@pytest.mark.parametrize("name", ["intree", "valid", "msglen", "longmsg", "adversarial", "lattice_edge"])
 def test_cpu_path_matches_golden(sv, golden, name):
     d = golden[name]
     out = sv.verify_batch_cpu(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"], threads=4)

@@ -367,3 +367,58 @@ def test_checkpoint_prefetch_1m_signatures(sv, dev):
     h, m = ctypes.c_uint64(), ctypes.c_uint64()
     host.svh_cache_counts(ctypes.byref(h), ctypes.byref(m))
     assert h.value == 0 and m.value == 0  # the verify cache was bypassed
+
+
+# ------------------------------------------------ slot-table lifetime
+def test_remap_and_shutdown_under_concurrent_calls(sv, dev, golden):
+    """sv_set_device_map / sv_shutdown while four threads verify on every
+    slot (host batches on both kernel paths and device batches): each call
+    either waits for the re-map or runs before it, so every verdict is
+    libsodium's and no call fails (include/stellar_sigverify.h: all entry
+    points are thread-safe, including against teardown).  The CPU-side form
+    of this race runs under ThreadSanitizer in tools/tsan_host.sh."""
+    lib = sv.load_library()
+    d = golden["adversarial"]
+    tpk, tsig, tm = random_dataset(sv, dev, 20000, 91)
+    stop = threading.Event()
+    errors, counts = [], [0] * 4
+
+    def worker(k):
+        st = torch.cuda.Stream(dev)
+        tv = torch.zeros(20000, dtype=torch.uint8, device=dev)
+        try:
+            while not stop.is_set():
+                if k == 3:
+                    with torch.cuda.stream(st):
+                        sv.verify_device(0, tpk.data_ptr(), tsig.data_ptr(), tm.data_ptr(), 20000, tv.data_ptr(),
+                                         stream=st.cuda_stream)
+                    st.synchronize()
+                    assert int(tv.sum(dtype=torch.int64).item()) == 20000
+                else:
+                    out = sv.verify_batch(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"],
+                                          path=("latency", "throughput", None)[k])
+                    assert np.array_equal(out, d["verdict"])
+                counts[k] += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+            stop.set()
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    try:
+        for r in range(12):
+            if stop.is_set():
+                break
+            if r % 3 == 2:
+                lib.sv_shutdown()
+            else:
+                sv.set_device_map([0] * (1 + r % 2))
+            threading.Event().wait(0.15)
+    finally:
+        stop.set()
+        for t in th:
+            t.join(timeout=120)
+        sv.set_device_map([])
+    assert not errors, errors
+    assert min(counts) > 0, counts

@@ -40,7 +40,7 @@ def test_intree_vectors_expected_verdicts(oracle, golden):
     assert (got == d["verdict"]).all()
 
 
-@pytest.mark.parametrize("name", ["valid", "msglen", "adversarial", "lattice_edge"])
+@pytest.mark.parametrize("name", ["valid", "msglen", "longmsg", "adversarial", "lattice_edge"])
 def test_oracle_matches_libsodium_golden(oracle, golden, name):
     d = golden[name]
     got = oracle_verdicts(oracle, d)

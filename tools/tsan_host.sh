@@ -86,3 +86,17 @@ PY
 TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$(gcc -print-file-name=libtsan.so) \
     python3 $O/txset.py $O/libstellar_host.so "$R/tests/native/libhostcore.so" "$R" > $O/out_txset.txt 2>&1 || true
 echo "tx-set pre-pass + keyed walk: TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out_txset.txt || true); result: $(tail -1 $O/out_txset.txt)"
+# the C-ABI's slot-table lifetime (sv_shutdown / sv_set_device_map against
+# in-flight calls on stub slots): sv_api.cpp instrumented, the kernel objects
+# as built
+O2=/tmp/tsan_life
+mkdir -p $O2
+R2=$R/stellar-core_amd
+/opt/rocm/bin/hipcc -O1 -g -std=c++17 -fPIC -Xarch_host -fsanitize=thread -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include \
+    -c $R2/csrc/sv_api.cpp -o $O2/sv_api_tsan.o
+/opt/rocm/bin/hipcc -O1 -g -std=c++17 -Xarch_host -fsanitize=thread -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include \
+    -c $R/tools/tsan_lifetime.cpp -o $O2/tsan_lifetime.o
+/opt/rocm/bin/hipcc -Xarch_host -fsanitize=thread --offload-arch=gfx950 -o $O2/tsan_lifetime $O2/tsan_lifetime.o $O2/sv_api_tsan.o \
+    $R2/build/sv_kernels.o $R2/build/sv_comb.o $R2/build/sv_hash.o $R2/build/sv_cpu.o -Wl,-rpath,/opt/rocm/lib -lpthread
+TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" $O2/tsan_lifetime > $O2/out_life.txt 2>&1 || true
+echo "slot lifetime (4 callers vs remap/shutdown): TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O2/out_life.txt || true); result: $(tail -1 $O2/out_life.txt)"
