@@ -134,10 +134,13 @@ int sv_ed25519_verify_batch_gather_cb(const uint8_t* const* pk, const uint8_t* c
  * As sv_ed25519_verify_batch_gather_cb, with the keys delivered in pieces:
  * keys_ready(ctx, ready) runs with keys [0, ready) in `keys`, for increasing
  * `ready`, the last time with ready == n.  For a one-chunk batch of >= 8192
- * signatures the engine packs, copies up and hashes the batch in 4 pieces, so
- * a caller that walks its cache in item order (verifySigBatch,
- * /root/reference/src/crypto/SecretKey.cpp:446-466 per item) starts on the
- * first quarter while the rest is still on its way.  Same threading rules.
+ * signatures the engine packs, copies up and hashes the batch in pieces: the
+ * first of 2048 rows, each later one twice the one before, at most 32768 rows,
+ * and no runt last piece (a remainder under 1.5 pieces joins the one before;
+ * a 100k batch is 6 pieces).  So a caller that walks its cache in item order
+ * (verifySigBatch, /root/reference/src/crypto/SecretKey.cpp:446-466 per item)
+ * starts on the first rows while the rest is still on its way.  Same threading
+ * rules.
  */
 int sv_ed25519_verify_batch_gather_progress(const uint8_t* const* pk, const uint8_t* const* sig,
                                             const uint8_t* const* msg, const uint32_t* msg_len, size_t n,

@@ -27,7 +27,7 @@
 
 #define SV_CE_DW 48          // dwords per entry: 4 coordinates x 12
 #define SV_KA_POS 64         // -A tables: positions j (weight 16^j)
-#define SV_KA_ENT 9          //   entries d = 0..8 (signed digits in [-8, 7])
+#define SV_KA_ENT 9          //   entries |d| = 0..8 (signed radix-16 digits in [-8, 8])
 #define SV_KEY_SLOT_DW (SV_KA_POS * SV_KA_ENT * SV_CE_DW)  // 27648 dwords = 108 KiB per key
 #define SV_CB_POS 32         // B tables: positions j (weight 256^j)
 #define SV_CB_ENT 129        //   entries e = 0..128 (signed digits in [-128, 127])

@@ -12,6 +12,8 @@
 #include <chrono>
 #include <functional>
 #include <limits>
+#include <condition_variable>
+#include <exception>
 #include <mutex>
 #include <random>
 #include <string>
@@ -734,13 +736,42 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
       // how many keys are in (the engine delivers them in pieces); this thread
       // walks the cache as they land -- the thread whose caches hold the
       // verify cache from earlier calls.
+      // Once there is nothing to walk or pre-draw, this thread sleeps on `cv`
+      // (after a short spin: a piece of keys is usually close) instead of
+      // holding a core for the whole engine call.  An exception on the engine
+      // thread is carried over and rethrown here after the join; the join
+      // also runs when this thread's walk throws (EngJoin).
       std::atomic<size_t> ready{0};
       std::atomic<bool> fin{false};
-      std::function<void(size_t)> publish = [&](size_t r) { ready.store(r, std::memory_order_release); };
+      std::mutex wm;
+      std::condition_variable cv;
+      std::exception_ptr engExc;
+      std::function<void(size_t)> publish = [&](size_t r) {
+        {
+          std::lock_guard<std::mutex> lk(wm);
+          ready.store(r, std::memory_order_release);
+        }
+        cv.notify_one();
+      };
       std::thread eng([&] {
-        erc = timedBatch(true, E, [&] { return gpuVerify(items, rows, verdict.data(), keys.data(), &publish, &sc); });
-        fin.store(true, std::memory_order_release);
+        try {
+          erc = timedBatch(true, E, [&] { return gpuVerify(items, rows, verdict.data(), keys.data(), &publish, &sc); });
+        } catch (...) {
+          engExc = std::current_exception();
+          erc = SV_ERR_INVALID_ARG;
+        }
+        {
+          std::lock_guard<std::mutex> lk(wm);
+          fin.store(true, std::memory_order_release);
+        }
+        cv.notify_one();
       });
+      struct EngJoin {
+        std::thread& t;
+        ~EngJoin() {
+          if (t.joinable()) t.join();
+        }
+      } engJoin{eng};
       size_t drawn = 0;
       for (;;) {
         const bool f = fin.load(std::memory_order_acquire);
@@ -763,9 +794,16 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
           if (drawn == before) drawn = E;  // (nothing more to queue)
           continue;
         }
-        std::this_thread::yield();
+        // nothing to do until the next piece or the end of the engine call
+        const auto spinEnd = std::chrono::steady_clock::now() + std::chrono::microseconds(20);
+        while (ready.load(std::memory_order_acquire) <= done && !fin.load(std::memory_order_acquire) &&
+               std::chrono::steady_clock::now() < spinEnd)
+          std::this_thread::yield();
+        std::unique_lock<std::mutex> lk(wm);
+        cv.wait(lk, [&] { return ready.load(std::memory_order_acquire) > done || fin.load(std::memory_order_acquire); });
       }
       eng.join();
+      if (engExc) std::rethrow_exception(engExc);
     } else {
       erc = timedBatch(true, E, [&] { return gpuVerify(items, rows, verdict.data(), keys.data(), &phase1, &sc); });
     }

@@ -173,9 +173,10 @@ __global__ __launch_bounds__(256, 1) void sv_comb_kernel(sv_comb_params c) {
   uint32_t h[8], dA[8], dB[8];
   sc_reduce512(h, hram);
   const bool s_ok = sc_is_canonical(S);
-  // a lane with S >= L is rejected by (1); masking S's top nibble keeps its
-  // radix-256 digits inside the table ([-128, 127]); a no-op for S < L
-  S[7] &= 0x0fffffffu;
+  // a lane with S >= L is rejected by (1); clearing bits 253..255 keeps its
+  // radix-256 digits inside the table (top digit <= 32); every S < 2^253,
+  // so every S < L, is left unchanged
+  S[7] &= 0x1fffffffu;
   sc_digits_r16(dA, h);
   sc_digits_r256(dB, S);
 

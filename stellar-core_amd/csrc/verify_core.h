@@ -313,12 +313,12 @@ SV_HD bool sv_verify_pre(ge_p3& P, const uint32_t A[8], const sv_u4* Rp, const u
   ok = ge_frombytes(negA, A, true) && ok;
   uint32_t h[8];
   sc_reduce512(h, hram);
-  // Lanes with S >= L are already rejected by (1); masking S's top nibble keeps
-  // their radix-256 recoding inside [-128, 127] (table bounds).  For every
-  // lane that can be accepted (S < L < 2^253) the mask is a no-op.
+  // Lanes with S >= L are already rejected by (1); clearing bits 253..255
+  // keeps their recoding inside the table bounds.  Every S < 2^253 (so every
+  // S < L, the lanes that can be accepted) is left unchanged.
   uint32_t Sc[8];
   SV_UNROLL for (int i = 0; i < 8; ++i) Sc[i] = S[i];
-  Sc[7] &= 0x0fffffffu;
+  Sc[7] &= 0x1fffffffu;
   sv_double_scalarmult<STAGED>(P, negA, h, Sc, slot, qstride, btab, stage);
   if (!ok) fe_1(P.Z);
   return ok;

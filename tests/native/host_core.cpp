@@ -340,7 +340,7 @@ static bool comb_verify_one(const uint32_t* ktab, uint32_t kst, const uint8_t* p
   sha512_ram_var(hram, R, A, msg, mlen);
   sc_reduce512(h, hram);
   const bool s_ok = sc_is_canonical(S);
-  S[7] &= 0x0fffffffu;
+  S[7] &= 0x1fffffffu;  // (bits 253..255: S >= L is rejected by (1); every S < 2^253 unchanged)
   sc_digits_r16(dA, h);
   sc_digits_r256(dB, S);
   ge_p3 P;
@@ -386,6 +386,31 @@ static bool comb_verify_one(const uint32_t* ktab, uint32_t kst, const uint8_t* p
   fe_mul(t, Rp.Y, P.Z);
   fe_sub(dy, P.Y, t);
   return fe_iszero(dx) && fe_iszero(dy) && r_ok && s_ok && kst == SV_KEY_OK;
+}
+
+// [S]B through the comb base tables exactly as comb_verify_one computes it
+// (the mask of S's bits 253..255, the signed radix-256 recoding, 32 entries),
+// encoded: pins the base half for scalars S in [2^252, L), which no valid
+// signature can be built to reach.
+extern "C" void hc_comb_base_mul(const uint8_t s_bytes[32], uint8_t out[32]) {
+  std::call_once(g_cb_once, init_cb);
+  uint32_t S[8], dB[8];
+  load_words(S, s_bytes);
+  S[7] &= 0x1fffffffu;
+  sc_digits_r256(dB, S);
+  ge_p3 P;
+  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
+  ge_p1p1 Q;
+  for (int j = 0; j < SV_CB_POS; ++j) {
+    const int32_t e = (int32_t)(dB[j >> 2] << (24 - 8 * (j & 3))) >> 24;
+    ge_cached c;
+    sv_ce_get(c, &g_cb[((size_t)j * SV_CB_ENT + (uint32_t)(e < 0 ? -e : e)) * SV_CE_DW], e < 0);
+    ge_add_preswapped(Q, P, c.YpX, c.YmX, c.Z, c.T2d, e < 0, false);
+    ge_p1p1_to_p3(P, Q);
+  }
+  uint32_t enc[8];
+  ge_p2_tobytes(enc, P.X, P.Y, P.Z);
+  memcpy(out, enc, 32);
 }
 
 extern "C" void hc_comb_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,

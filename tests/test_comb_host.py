@@ -40,3 +40,58 @@ def test_key_index_fuzz(hostcore, seed, cap, ops, universe):
     f = hostcore.hc_keyindex_fuzz
     f.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     assert f(seed, cap, ops, universe) == 0
+
+
+def test_comb_base_half_top_scalars(hostcore):
+    """the comb path masks S before its radix-256 recoding.  The
+    mask must leave every S < L unchanged, including S in [2^252, L) (bit 252
+    set), which no valid signature can be constructed to reach (S = r + h a
+    with h bound to R and A).  [S]B from the comb base tables against a plain
+    Python scalar multiplication."""
+    P = 2**255 - 19
+    L = 2**252 + 27742317777372353535851937790883648493
+    D = (-121665 * pow(121666, P - 2, P)) % P
+
+    def add(p, q):  # extended coordinates, a = -1
+        X1, Y1, Z1, T1 = p
+        X2, Y2, Z2, T2 = q
+        A = (Y1 - X1) * (Y2 - X2) % P
+        B = (Y1 + X1) * (Y2 + X2) % P
+        C = 2 * D * T1 * T2 % P
+        Dd = 2 * Z1 * Z2 % P
+        E, F, G, H = B - A, Dd - C, Dd + C, B + A
+        return (E * F % P, G * H % P, F * G % P, E * H % P)
+
+    def mul(k, p):
+        r = (0, 1, 1, 0)
+        while k:
+            if k & 1:
+                r = add(r, p)
+            p = add(p, p)
+            k >>= 1
+        return r
+
+    def enc(p):
+        X, Y, Z, _ = p
+        zi = pow(Z, P - 2, P)
+        x, y = X * zi % P, Y * zi % P
+        return (y | ((x & 1) << 255)).to_bytes(32, "little")
+
+    by = 4 * pow(5, P - 2, P) % P
+    x2 = (by * by - 1) * pow(D * by * by + 1, P - 2, P) % P
+    bx = pow(x2, (P + 3) // 8, P)
+    if (bx * bx - x2) % P:
+        bx = bx * pow(2, (P - 1) // 4, P) % P
+    if bx & 1:
+        bx = P - bx
+    B = (bx, by, 1, bx * by % P)
+    f = hostcore.hc_comb_base_mul
+    f.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    rng = np.random.default_rng(252)
+    scalars = [L - 1, L - 2, 2**252, 2**252 + 1, 2**252 + 12345, 2**252 - 1, 1, 0]
+    scalars += [2**252 + int(rng.integers(0, 2**62)) * 2**60 % (L - 2**252) for _ in range(4)]
+    scalars += [int.from_bytes(rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), "little") % L for _ in range(4)]
+    for k in scalars:
+        out = ctypes.create_string_buffer(32)
+        f(k.to_bytes(32, "little"), out)
+        assert out.raw == enc(mul(k, B)), hex(k)

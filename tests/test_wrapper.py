@@ -196,3 +196,36 @@ def test_wrapper_fixtures_gpu(host, sv):
     finally:
         host.svh_set_cpu_threshold(1)
         host.svh_cache_clear()
+
+
+def test_fuzz_build_accepts_without_verifying(host, sv, tmp_path):
+    """FUZZING_BUILD_MODE_UNSAFE_FOR_PRODUCTION: the reference's checker
+    accepts every signature and reports every signature used
+    (SignatureChecker.cpp:34-36, 141-143).  The mirror built with the same
+    macro must do the same and verify nothing (no engine call, no pre-pass);
+    the normal build rejects the same corrupted set."""
+    import subprocess
+    src = os.path.join(REPO, "stellar-core_amd", "csrc", "host")
+    lib = tmp_path / "libstellar_host_fuzz.so"
+    files = [os.path.join(src, f + ".cpp") for f in ("hashes", "PubKeyUtils", "SignatureChecker",
+                                                     "VerifyMicroBatcher", "TransactionSignatures", "host_capi")]
+    subprocess.run(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-DFUZZING_BUILD_MODE_UNSAFE_FOR_PRODUCTION",
+                    "-o", str(lib)] + files + ["-L" + os.path.dirname(sv.LIB_PATH), "-lstellar_sigverify",
+                                                "-Wl,-rpath," + os.path.dirname(sv.LIB_PATH), "-lpthread"],
+                   check=True)
+    fz = ctypes.CDLL(str(lib))
+    fz.svh_last_error_string.restype = ctypes.c_char_p
+    rows = _pubkey_rows()[:20]
+    bad = []
+    for signers, sigs, h, needed in rows:
+        s = dict(sigs[0])
+        s["sig"] = bytes(64 - 1) + b"\x01"  # not a signature of anything
+        bad.append((signers, [s], h, needed))
+    for prefetch in (0, 1):
+        ok, used = _run_txset(host, bad, prefetch)
+        assert not ok.any() and not used.any()
+        before = engine_stats(fz)
+        ok, used = _run_txset(fz, bad, prefetch)
+        after = engine_stats(fz)
+        assert ok.all() and used.all()
+        assert (after.gpu_signatures, after.cpu_signatures) == (before.gpu_signatures, before.cpu_signatures)
