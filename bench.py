@@ -226,6 +226,28 @@ def config1(sv, sodium, spath, pk_h, sig_h, msgs, threads, device):
             "cpu_threads": threads, "single_thread_sample": st,
             "all_valid": bool(g_ok and o1.all() and o2.all() and o3.all() and o4.all()),
         }
+    # verify-hit benchmarking (CryptoTests.cpp:308-316: benchmarkOpsPerSecond
+    # with 10 passes, the last 9 timed, every call a cache hit): the mirror's
+    # PubKeyUtils::verifySig on the 10k x 256 B cases, 1 thread and 3 threads
+    # contending for the cache (native loop, include/stellar_host.h)
+    host = ctypes.CDLL(sv.HOSTLIB_PATH)
+    host.svh_bench_verify_hits.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    _, pk, sg, m, mlen, _ = shapes[1]
+    pk, sg, m = (np.ascontiguousarray(x) for x in (pk, sg, m))
+    hit = {"cases": int(pk.shape[0]), "msg_len": mlen, "passes": 10,
+           "what": "PubKeyUtils::verifySig mirror (BLAKE2b-256 key, 0xffff-entry random-eviction cache behind its "
+                   "mutex); pass 0 fills the cache (CPU-path verifies), passes 1-9 timed, all hits"}
+    for th in (1, 3):
+        host.svh_cache_clear()
+        rate, fill = ctypes.c_double(), ctypes.c_double()
+        rc = host.svh_bench_verify_hits(pk.ctypes.data, sg.ctypes.data, m.ctypes.data, mlen, pk.shape[0], 10, th,
+                                        ctypes.byref(rate), ctypes.byref(fill))
+        hit["hits_per_s_%dthread%s" % (th, "" if th == 1 else "s")] = rate.value
+        hit["fill_pass_s_%d" % th] = fill.value
+        hit["ok_%d" % th] = rc == 0
+    host.svh_cache_clear()
+    out["hit_path"] = hit
     return out
 
 

@@ -82,6 +82,18 @@ int svh_verify_sig(const uint8_t pk[32], const uint8_t* sig, size_t sig_len, con
 int svh_verify_sig_batch(const uint8_t* pk, const uint8_t* sig /* n x 64 */, const uint32_t* sig_len /* NULL = 64 */,
                          const uint8_t* msg, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
                          uint8_t* verdict);
+/* Verify-hit benchmark, the shape of the reference's "verify-hit benchmarking"
+ * (/root/reference/src/crypto/test/CryptoTests.cpp:308-316 ->
+ * SecretKey::benchmarkOpsPerSecond(.., 10000, 10), SecretKey.cpp:214-241):
+ * n cases (pk n x 32, sig n x 64, messages n x msg_len), one untimed pass of
+ * PubKeyUtils::verifySig over them (cache misses: verified and cached), then
+ * passes - 1 timed passes, every call a cache hit, on `threads` threads each
+ * walking all n cases from a different start (threads > 1: callers contending
+ * for the cache's mutex).  *hits_per_s = timed calls / timed wall seconds over
+ * all threads; *fill_s = the first pass's wall seconds.  Returns 0, or < 0 if
+ * any call did not return 1 (the cases must be valid). */
+int svh_bench_verify_hits(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, size_t msg_len, size_t n,
+                          int passes, int threads, double* hits_per_s, double* fill_s);
 void svh_cache_clear(void);
 void svh_cache_seed(unsigned int seed);
 void svh_cache_counts(uint64_t* hits, uint64_t* misses); /* flushes, like flushVerifySigCacheCounts */

