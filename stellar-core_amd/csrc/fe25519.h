@@ -110,49 +110,13 @@ SV_HD void fe_weak_even(fe& h) {
   }
 }
 
-// Sequential carry of 64-bit column sums into a carried fe (R).
-// Order interleaves two chains for ILP (0->1->2->3->4 and 4->5->...->9->0).
-#ifndef SV_CARRY_SINGLE
-#define SV_CARRY_SINGLE 1
-#endif
-SV_HD void fe_carry_wide(fe& out, uint64_t h[10]) {
-  uint64_t c;
-#if SV_CARRY_SINGLE
-  // one chain 0->1->...->9->0->1: 11 steps (VALU back-to-back dependent
-  // issue is free on CDNA, so the 12-step two-chain form buys no ILP)
-  SV_UNROLL for (int i = 0; i < 9; ++i) {
-    c = h[i] >> fe_width(i); h[i + 1] += c; h[i] &= fe_mask(i);
-  }
-  c = h[9] >> 25; h[0] += c * 19u; h[9] &= SV_M25;
-  c = h[0] >> 26; h[1] += c; h[0] &= SV_M26;
-  SV_UNROLL for (int i = 0; i < 10; ++i) out.v[i] = (uint32_t)h[i];
-  return;
-#endif
-  c = h[0] >> 26; h[1] += c; h[0] &= SV_M26;
-  c = h[4] >> 26; h[5] += c; h[4] &= SV_M26;
-  c = h[1] >> 25; h[2] += c; h[1] &= SV_M25;
-  c = h[5] >> 25; h[6] += c; h[5] &= SV_M25;
-  c = h[2] >> 26; h[3] += c; h[2] &= SV_M26;
-  c = h[6] >> 26; h[7] += c; h[6] &= SV_M26;
-  c = h[3] >> 25; h[4] += c; h[3] &= SV_M25;
-  c = h[7] >> 25; h[8] += c; h[7] &= SV_M25;
-  c = h[4] >> 26; h[5] += c; h[4] &= SV_M26;
-  c = h[8] >> 26; h[9] += c; h[8] &= SV_M26;
-  c = h[9] >> 25; h[0] += c * 19u; h[9] &= SV_M25;
-  c = h[0] >> 26; h[1] += c; h[0] &= SV_M26;
-  SV_UNROLL for (int i = 0; i < 10; ++i) out.v[i] = (uint32_t)h[i];
-}
-
 // One 32x32->64 multiply-accumulate = one v_mad_u64_u32.  Written as inline
 // asm so the multiplicands are guaranteed 32-bit VGPRs: with plain C, LLVM
 // promotes limbs merged across branches to i64 and the backend then emits
 // 64x32-bit products (2 v_mad_u64_u32 + 2 v_mov each).  The carry-out SGPR
 // pair is architecturally required on gfx950 (no `null` sdst); vcc is used
 // and never read.
-#ifndef SV_MAD_ASM
-#define SV_MAD_ASM 1
-#endif
-// Carry-out SGPR pairs the inline-asm mads rotate over (SV_MAD_PAIRS > 0):
+// Carry-out SGPR pairs the inline-asm mads rotate over (SV_MAD_PAIRS):
 // a VALU write of the SAME SGPR pair by consecutive mads serialises them
 // (tools/ubench_valu.hip: 9.5 vs 6.4 cycles per wave-instruction at one wave
 // per SIMD), so product k writes pair k mod SV_MAD_PAIRS from the top of the
@@ -177,7 +141,7 @@ SV_HD void fe_carry_wide(fe& out, uint64_t h[10]) {
     default: M(80, 81); break; \
   }
 SV_HD void sv_mad_init_k(uint64_t& acc, uint32_t a, uint32_t b, int k) {
-#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
+#if defined(__HIP_DEVICE_COMPILE__)
   SV_MAD_SWITCH(SV_MAD_I)
 #else
   (void)k;
@@ -185,7 +149,7 @@ SV_HD void sv_mad_init_k(uint64_t& acc, uint32_t a, uint32_t b, int k) {
 #endif
 }
 SV_HD void sv_mad_k(uint64_t& acc, uint32_t a, uint32_t b, int k) {
-#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
+#if defined(__HIP_DEVICE_COMPILE__)
   SV_MAD_SWITCH(SV_MAD_A)
 #else
   (void)k;
@@ -195,62 +159,13 @@ SV_HD void sv_mad_k(uint64_t& acc, uint32_t a, uint32_t b, int k) {
 SV_HD void sv_mad_init(uint64_t& acc, uint32_t a, uint32_t b) { sv_mad_init_k(acc, a, b, 0); }
 SV_HD void sv_mad(uint64_t& acc, uint32_t a, uint32_t b) { sv_mad_k(acc, a, b, 0); }
 
-// Column sums of f*g (DBL: of 2*f*g).  Wrapped columns (i+j >= 10) carry the
-// factor 2^255 = 19 on g; odd*odd products carry an extra 2 (half-bit radix).
-template <bool DBL>
-SV_HD void fe_mul_cols(uint64_t h[10], const fe& f, const fe& g) {
-  uint32_t g19[10], fa[10], fb[10];
-  SV_UNROLL for (int j = 0; j < 10; ++j) g19[j] = 19u * g.v[j];
-  SV_UNROLL for (int i = 0; i < 10; ++i) {
-    fa[i] = DBL ? (f.v[i] << 1) : f.v[i];       // multiplier when not odd*odd
-    fb[i] = DBL ? (f.v[i] << 2) : (f.v[i] << 1);  // multiplier for odd*odd
-  }
-  SV_UNROLL for (int i = 0; i < 10; ++i) {
-    SV_UNROLL for (int j = 0; j < 10; ++j) {
-      const int k = i + j;
-      const uint32_t a = ((i & 1) && (j & 1)) ? fb[i] : fa[i];
-      const uint32_t b = (k >= 10) ? g19[j] : g.v[j];
-      if (i == 0) sv_mad_init_k(h[k], a, b, 10 * i + j);  // i == 0 opens every column
-      else sv_mad_k(h[k >= 10 ? k - 10 : k], a, b, 10 * i + j);
-    }
-  }
-}
-
-#ifndef SV_SQ_ASM
-#define SV_SQ_ASM 1
-#endif
-// Column sums of f^2 (DBL: 2 f^2), using the symmetry f_i f_j = f_j f_i.
-template <bool DBL>
-SV_HD void fe_sq_cols(uint64_t h[10], const fe& f) {
-  SV_UNROLL for (int i = 0; i < 10; ++i) {
-    SV_UNROLL for (int j = i; j < 10; ++j) {
-      const int k = i + j;
-      const int sh = (i != j ? 1 : 0) + (((i & 1) && (j & 1)) ? 1 : 0) + (DBL ? 1 : 0);
-      const uint32_t a = f.v[i] << sh;
-      const uint32_t b = (k >= 10) ? 19u * f.v[j] : f.v[j];
-#if SV_SQ_ASM
-      if (i == 0) sv_mad_init_k(h[k], a, b, 10 * i + j);
-      else sv_mad_k(h[k >= 10 ? k - 10 : k], a, b, 10 * i + j);
-#else
-      // plain C here: squaring operands are never phi-merged, so LLVM keeps
-      // them 32-bit, and compiler-emitted mads need no hazard s_nops
-      if (i == 0) h[k] = (uint64_t)a * b;  // i == 0 opens every column
-      else h[k >= 10 ? k - 10 : k] += (uint64_t)a * b;
-#endif
-    }
-  }
-}
-
 // Column-major forms with the carry chain folded into the multiply-adds:
 // column k (terms i + j = k and i + j = k + 10) is opened by a mad whose
 // addend is the carry out of column k - 1, so each carry step is one 64-bit
-// shift and one mask; the separate 64-bit add of fe_carry_wide is gone (9 of
-// them per product).  The price is one dependent chain per product instead of
+// shift and one mask, and no separate 64-bit add per column (9 fewer per
+// product than summing the columns first and carrying after).  The price is one dependent chain per product instead of
 // ten interleaved accumulators.  Bounds: the carry (< 2^38) adds nothing
 // measurable to a column sum (< 2^62.8), and the output is R as above.
-#ifndef SV_COLMAJOR
-#define SV_COLMAJOR 1
-#endif
 // One column as ONE inline-asm statement (z: the first mad opens with 0, a:
 // with acc).  Per-mad statements cost an s_nop between every two dependent
 // ones: LLVM's gfx950 hazard recognizer assumes any inline asm may carry the
@@ -259,7 +174,7 @@ SV_HD void fe_sq_cols(uint64_t h[10], const fe& f) {
 // state.  Inside one statement the mads issue back to back; a dependent chain
 // costs nothing extra on gfx950 (tools/ubench_valu_rates: dependency distance
 // 1, 2 and 4 issue at the independent rate).
-#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
+#if defined(__HIP_DEVICE_COMPILE__)
 SV_HD void sv_col10_z(uint64_t& acc, const uint32_t a[10], const uint32_t b[10]) {
   asm(
       "v_mad_u64_u32 %0, s[94:95], %1, %11, 0\n"
@@ -373,7 +288,7 @@ SV_HD void fe_mul_cm(fe& h, const fe& f, const fe& g) {
   }
   uint64_t acc = 0, c = 0;
   SV_UNROLL for (int k = 0; k < 10; ++k) {
-#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
+#if defined(__HIP_DEVICE_COMPILE__)
     uint32_t A[10], B[10];
     SV_UNROLL for (int i = 0; i < 10; ++i) {
       const int j = (k - i + 10) % 10;
@@ -425,7 +340,7 @@ SV_HD void fe_sq_cm(fe& h, const fe& f) {
         A[t] = a;
         B[t] = b;
         ++t;
-#if !(defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM)
+#if !defined(__HIP_DEVICE_COMPILE__)
         if (first) sv_mad_open(acc, c, a, b, k, n);
         else sv_mad_k(acc, a, b, n);
 #endif
@@ -433,7 +348,7 @@ SV_HD void fe_sq_cm(fe& h, const fe& f) {
         ++n;
       }
     }
-#if defined(__HIP_DEVICE_COMPILE__) && SV_MAD_ASM
+#if defined(__HIP_DEVICE_COMPILE__)
     // columns hold 6 terms (k even) or 5 (k odd)
     if (k == 0) {
       sv_col6_z(acc, A, B);
@@ -451,13 +366,10 @@ SV_HD void fe_sq_cm(fe& h, const fe& f) {
   h = out;
 }
 
-// SV_FE_ASM (device): each product / square as one generated inline-asm
+// Device: each product / square as one generated inline-asm
 // statement (fe_asm_gen.h, tools/gen_fe_asm.py), same arithmetic as the
 // column-major forms above.
-#ifndef SV_FE_ASM
-#define SV_FE_ASM 1
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && SV_FE_ASM && SV_COLMAJOR && SV_MAD_ASM
+#if defined(__HIP_DEVICE_COMPILE__)
 #define SV_FE_ASM_ON 1
 #include "fe_asm_gen.h"
 #else
@@ -489,12 +401,8 @@ SV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   SV_MADS(SV_MADS_MUL);
 #if SV_FE_ASM_ON
   fe_mul_asm(h, f, g);
-#elif SV_COLMAJOR
-  fe_mul_cm<false>(h, f, g);
 #else
-  uint64_t c[10];
-  fe_mul_cols<false>(c, f, g);
-  fe_carry_wide(h, c);
+  fe_mul_cm<false>(h, f, g);
 #endif
   SV_FENCE();
 }
@@ -518,12 +426,8 @@ SV_HD void fe_mul2(fe& h, const fe& f, const fe& g) {
   SV_MADS(SV_MADS_MUL);
 #if SV_FE_ASM_ON
   fe_mul2_asm(h, f, g);
-#elif SV_COLMAJOR
-  fe_mul_cm<true>(h, f, g);
 #else
-  uint64_t c[10];
-  fe_mul_cols<true>(c, f, g);
-  fe_carry_wide(h, c);
+  fe_mul_cm<true>(h, f, g);
 #endif
   SV_FENCE();
 }
@@ -531,12 +435,8 @@ SV_HD void fe_sq(fe& h, const fe& f) {
   SV_MADS(SV_MADS_SQ);
 #if SV_FE_ASM_ON
   fe_sq_asm(h, f);
-#elif SV_COLMAJOR
-  fe_sq_cm<false>(h, f);
 #else
-  uint64_t c[10];
-  fe_sq_cols<false>(c, f);
-  fe_carry_wide(h, c);
+  fe_sq_cm<false>(h, f);
 #endif
   SV_FENCE();
 }
@@ -545,12 +445,8 @@ SV_HD void fe_sq2(fe& h, const fe& f) {
   SV_MADS(SV_MADS_SQ);
 #if SV_FE_ASM_ON
   fe_sq2_asm(h, f);
-#elif SV_COLMAJOR
-  fe_sq_cm<true>(h, f);
 #else
-  uint64_t c[10];
-  fe_sq_cols<true>(c, f);
-  fe_carry_wide(h, c);
+  fe_sq_cm<true>(h, f);
 #endif
   SV_FENCE();
 }
@@ -559,12 +455,8 @@ SV_HD void fe_sq2(fe& h, const fe& f) {
 // registers distinct from its inputs, so a one-squaring loop copies its 10
 // limbs back into the loop-carried registers every iteration (10 v_mov per
 // squaring); with two the second squaring writes straight into them.
-#ifndef SV_SQN_PAIRS
-#define SV_SQN_PAIRS 1
-#endif
 SV_HD void fe_sqn(fe& h, const fe& f, int n) {
   fe_sq(h, f);
-#if SV_SQN_PAIRS
   int i = 1;
   if ((n - 1) & 1) {  // (n is a constant at every call site: folded)
     fe_sq(h, h);
@@ -575,9 +467,6 @@ SV_HD void fe_sqn(fe& h, const fe& f, int n) {
     fe_sq(t, h);
     fe_sq(h, t);
   }
-#else
-  SV_NOUNROLL for (int i = 1; i < n; ++i) fe_sq(h, h);
-#endif
 }
 
 // h = cond ? f : h  (per lane, branch-free)

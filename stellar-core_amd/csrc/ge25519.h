@@ -24,17 +24,8 @@
 #include "fe25519.h"
 
 
-#ifndef SV_DBL_WEAK_EVEN
-#define SV_DBL_WEAK_EVEN 1
-#endif
-#ifndef SV_SHARE_T19
-#define SV_SHARE_T19 1
-#endif
 // p1p1 -> p3: Y is the g operand of both Y3 = Z Y and T3 = X Y, so its
 // 19-multiples are computed once as well (9 v_mul_lo_u32 per conversion)
-#ifndef SV_SHARE_Y19
-#define SV_SHARE_Y19 1
-#endif
 
 struct ge_p2 { fe X, Y, Z; };
 struct ge_p3 { fe X, Y, Z, T; };
@@ -64,11 +55,7 @@ SV_HD void ge_dbl(ge_p1p1& r, const fe& X, const fe& Y, const fe& Z) {
   fe_sub(r.Z, YY, XX);    // y^2 - x^2            M3
   fe_sub4(r.X, AA, r.Y);  // 2xy = (x+y)^2 - ..  M5
   fe_sub4(r.T, ZZ2, r.Z); // 2z^2 - (y^2 - x^2)  M5
-#if SV_DBL_WEAK_EVEN
   fe_weak_even(r.T);      // T is only ever a conversion product's g operand
-#else
-  fe_weak(r.T);           // R+
-#endif
 }
 
 // p1p1 -> p3 (wantT) or -> p2 (T left stale).  r must not alias p.  Bounds:
@@ -76,7 +63,6 @@ SV_HD void ge_dbl(ge_p1p1& r, const fe& X, const fe& Y, const fe& Z) {
 // g operands whose 19-multiples are shared: Y by Z Y and X Y, T by X T and
 // Z T.
 SV_HD void ge_p1p1_convert(ge_p3& r, const ge_p1p1& p, bool wantT) {
-#if SV_SHARE_T19 && SV_SHARE_Y19
   {
     fe19 y19;
     fe_premul19(y19, p.Y);
@@ -87,19 +73,6 @@ SV_HD void ge_p1p1_convert(ge_p3& r, const ge_p1p1& p, bool wantT) {
   fe_premul19(t19, p.T);
   fe_mul_g19(r.X, p.X, p.T, t19);
   fe_mul_g19(r.Z, p.Z, p.T, t19);
-#elif SV_SHARE_T19
-  if (wantT) fe_mul(r.T, p.X, p.Y);
-  fe19 t19;
-  fe_premul19(t19, p.T);
-  fe_mul_g19(r.X, p.X, p.T, t19);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul_g19(r.Z, p.Z, p.T, t19);
-#else
-  if (wantT) fe_mul(r.T, p.X, p.Y);
-  fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul(r.Z, p.Z, p.T);
-#endif
 }
 
 SV_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {

@@ -111,9 +111,6 @@ struct sv_lat {
 #define SV_LAT_MAX_ITERS 400  // > 1.45 * 256 (worst-case Euclid length)
 
 // 1: Lehmer steps (below); 0: one 256-bit step per quotient only.
-#ifndef SV_LEHMER
-#define SV_LEHMER 1
-#endif
 
 // d = u*x - v*y over 8 words (u, v < 2^32); returns true iff the exact value
 // is negative (the values combined here are always within (-2^256, 2^256)).
@@ -235,7 +232,6 @@ SV_COLD void sc_lattice_reduce(sv_lat& o, const uint32_t h[8], bool trivial = fa
     uint32_t hi = 0;
     SV_UNROLL for (int i = SV_LAT_SPLIT_WORDS; i < 8; ++i) hi |= b[i];
     if (hi == 0) break;
-#if SV_LEHMER
     if (sv_lehmer_step(a, b, ta, tb, bneg)) {
       if (sv_lt8(a, b)) {  // (a quotient rounded low)
         SV_UNROLL for (int i = 0; i < 8; ++i) {
@@ -249,7 +245,6 @@ SV_COLD void sc_lattice_reduce(sv_lat& o, const uint32_t h[8], bool trivial = fa
       }
       continue;
     }
-#endif
     // one exact Euclid step (a >= b)
     const double qd = sv_words_to_double(a) / sv_words_to_double(b) * (1.0 - 0x1p-40);
     if (qd >= 4294967295.0) {  // (probability ~2^-32 per step) use (h, 1)

@@ -78,11 +78,7 @@ __device__ __forceinline__ void qd_dbl(ge_p3& P, const qd_role& q, bool wantT) {
   fe_sub(r.Z, YY, XX);
   fe_sub4(r.X, AA, r.Y);
   fe_sub4(r.T, ZZ2, r.Z);
-#if SV_DBL_WEAK_EVEN
   fe_weak_even(r.T);  // (T: a conversion product's g operand only)
-#else
-  fe_weak(r.T);
-#endif
   qd_p1p1_to_p3(P, r, q, wantT);
 }
 
@@ -173,11 +169,7 @@ __device__ __forceinline__ void qo_dbl(fe& h, const qd_role& q) {
   fe_sub(Zp, YY, XX);   // y^2 - x^2            M3
   fe_sub4(Xp, u, Yp);   // 2xy (lanes 0, 3)     M5
   fe_sub4(Tp, w, Zp);   // (lanes 0, 2)         M5
-#if SV_DBL_WEAK_EVEN
   fe_weak_even(Tp);  // (T: a conversion product's g operand only)
-#else
-  fe_weak(Tp);
-#endif
   // lane 0 X'T', 1 Y'Z', 2 Z'T', 3 X'Y' (p1p1 X is always the f operand)
   fe f, g;
   SV_UNROLL for (int i = 0; i < 10; ++i) {

@@ -56,11 +56,8 @@ SV_HD uint64_t sv_rotr64(uint64_t x, int n) {
 // maj(a, b, c) = bfi(a ^ b, c, b): where a and b differ c decides.  LLVM
 // canonicalises every C spelling of this back to and/or/xor (4 ops per half),
 // so the device form is one v_bfi_b32 per half.
-#ifndef SV_SHA_MAJ_BFI
-#define SV_SHA_MAJ_BFI 1
-#endif
 SV_HD uint64_t sv_maj64(uint64_t a, uint64_t b, uint64_t c) {
-#if defined(__HIP_DEVICE_COMPILE__) && SV_SHA_MAJ_BFI
+#if defined(__HIP_DEVICE_COMPILE__)
   const uint64_t x = a ^ b;
   uint32_t lo, hi;
   asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(lo) : "v"((uint32_t)x), "v"((uint32_t)c), "v"((uint32_t)b));

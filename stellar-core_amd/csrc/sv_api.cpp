@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -1298,6 +1299,9 @@ bool lat_trace() {
   return v != 0;
 }
 
+// Host-side stages of this thread's last latency-lane batch (sv_lat_last_trace).
+thread_local std::array<double, 8> t_lat_last{};
+
 // One latency-bound host batch on the slot's latency lane: pinned image (+
 // the key slots when warm), one H2D, [hash kernel, keys D2H], the comb kernel
 // (every key cached) or the octet kernel, one D2H, one sync.
@@ -1383,11 +1387,13 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   if (keys && !early) std::memcpy(keys, ho + (verdict ? n : 0), 32 * n);
   if (warm) ++L.warm;
   else ++L.cold;
+  const auto t2 = std::chrono::steady_clock::now();
+  auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::micro>(b - a).count();
+  };
+  t_lat_last = {us(t0, t1), us(t1, t_up), us(t_up, t_k), us(t_k, t_down), us(t_down, t_b), us(t_b, t2), us(t0, t2),
+                warm ? 1.0 : 0.0};
   if (lat_trace()) {
-    const auto t2 = std::chrono::steady_clock::now();
-    auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-      return std::chrono::duration<double, std::micro>(b - a).count();
-    };
     fprintf(stderr,
             "SV_LAT_TRACE n=%zu %s plan+pack %.1f us | h2d call %.1f launch %.1f d2h+rec %.1f build %.1f sync %.1f"
             " | device %.1f us\n",
@@ -1863,6 +1869,12 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
     return rc;
   SV_HIP(hipEventRecord(D.dep_out, D.stream));
   SV_HIP(hipStreamWaitEvent(user, D.dep_out, 0));
+  return SV_OK;
+}
+
+int sv_lat_last_trace(double out[8]) {
+  if (!out) return SV_ERR_INVALID_ARG;
+  for (int k = 0; k < 8; ++k) out[k] = t_lat_last[k];
   return SV_OK;
 }
 

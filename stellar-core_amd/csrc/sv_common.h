@@ -12,20 +12,13 @@
 #include <hip/hip_runtime.h>
 #define SV_HD __host__ __device__ __forceinline__
 // SV_COLD marks the once-per-signature phases (exponentiation chains,
-// decompression, mod-L reduction, Euclid, table build).  With SV_COLD_INLINE
-// (default) they are inlined like everything else: out of line, their array
+// decompression, mod-L reduction, Euclid, table build).  They are inlined
+// like everything else: out of line, their array
 // and struct arguments travel through scratch memory at every call (the prep
 // kernel spent ~23 % of its wave time waiting on memory); inlined, the whole
 // per-signature path stays in registers: -4.7 % end-to-end measured, with no
 // measurable instruction-cache misses (SQC_ICACHE_MISSES / HITS < 0.03 %).
-#ifndef SV_COLD_INLINE
-#define SV_COLD_INLINE 1
-#endif
-#if SV_COLD_INLINE
 #define SV_COLD __host__ __device__ __forceinline__
-#else
-#define SV_COLD __host__ __device__ __noinline__
-#endif
 #define SV_CONST __constant__
 #else
 #define SV_HD static inline

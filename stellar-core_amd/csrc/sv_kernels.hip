@@ -10,8 +10,10 @@
 //       (quad.h); the warm-key kernel is sv_comb.hip
 //   sv_btab_init_kernel  the base-point tables (device init)
 //   sv_sign_kernel   the RFC 8032 signer (benchmark datasets)
-// Kernel variants retired in round 3 are kept, unbuilt, in
-// tools/variants/legacy_kernels.hip.txt.
+// Retired kernel forms (the direct 253-bit ladder, the unsplit verify kernel,
+// the one-quad latency kernel) and the compile-time switches that selected
+// them were removed in round 4 (tools/unifdef.py; the shipped code objects
+// were unchanged, tools/codeobj_digest.sh); they are in the git history.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -22,9 +24,6 @@
 #include "keytab.h"
 
 #define SV_BLOCK 256
-#ifndef SV_STAGE_A
-#define SV_STAGE_A 1  // table_A entries via LDS-DMA prefetch (verify_core.h)
-#endif
 #define SV_WAVES_PER_SIMD 2
 // sv_main_kernel runs at 3 waves/SIMD (168 VGPRs): with its digits streamed
 // from the record and one base address per staged entry it fits without
@@ -33,12 +32,7 @@
 #ifndef SV_MAIN_WAVES
 #define SV_MAIN_WAVES 3
 #endif
-// 1: verify through the half-size equation (lattice.h, ~130 doublings per
-// signature); 0: the direct 253-bit ladder (sv_verify_kernel below).
-#ifndef SV_LATTICE
-#define SV_LATTICE 1
-#endif
-// base-point tables in the device buffer: e·B, then (SV_LATTICE) e·(2^128 B)
+// base-point tables in the device buffer: e·B, then e·(2^128 B) (lattice.h)
 
 // test knobs (include/stellar_sigverify.h sv_set_debug_flags)
 #define SV_DBG_TRIVIAL_PAIR 1u  // every lane takes the fallback pair (h, 1)
@@ -68,7 +62,7 @@ __device__ unsigned long long sv_phase_cycles[8];
 #define SV_PHASE(k) ((void)0)
 #endif
 
-// ---------------------------------------------- split form (SV_SPLIT = 1)
+// ---------------------------------------------- throughput path: prep + main
 // The per-signature phases (SHA-512, checks, decompression, mod L, Euclid,
 // tables, digits) and the scalar multiplication run as two kernels over a
 // chunk of up to SV_CHUNK signatures:
@@ -84,9 +78,6 @@ __device__ unsigned long long sv_phase_cycles[8];
 // than the spills cost.
 // Workspace per signature of the chunk: SV_SLOT_QUADS_L quads of tables, then
 // (separate array) SV_REC_QUADS quads of digits/flags.
-#ifndef SV_SPLIT
-#define SV_SPLIT 1
-#endif
 #ifndef SV_PREP_WAVES
 #define SV_PREP_WAVES 3
 #endif
@@ -287,9 +278,6 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   SV_PHASE(4);
 }
 
-#ifndef SV_MAIN_TOPINIT
-#define SV_MAIN_TOPINIT 1
-#endif
 // The main kernel's scalar multiplication: the step machine of
 // sv_lat_scalarmult (verify_core.h, STAGED with one stage region) with the
 // digits streamed from the signature's record instead of held in registers
@@ -309,7 +297,6 @@ __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw,
   // current and next digit words (the word changes every 8 windows)
   uint32_t curA = rw[7], curR = rw[15], nxtA = rw[6], nxtR = rw[14];
   ge_p1p1 Q;
-#if SV_MAIN_TOPINIT
   {
     // Window W-1 (no doublings; above every base-point window), peeled: P is
     // the identity, so P + Q_A = Q_A is taken straight from the (pre-swapped)
@@ -343,10 +330,6 @@ __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw,
     ge_p1p1_to_p3_opt(P, Q, false);  // (a doubling comes next)
   }
   SV_NOUNROLL for (int w = W - 2; w >= 0; --w) {
-#else
-  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
-  SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
-#endif
     const int pos = w + 64 - W;  // (wave-uniform)
     if ((pos & 7) == 7 && w != W - 1) {
       curA = nxtA;
@@ -414,7 +397,7 @@ __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw,
 template <bool KT>
 __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cparams c) {
   const sv_kparams& p = c.k;
-  __shared__ sv_u4 s_stage[SV_BLOCK / 64][(SV_STAGE_ONE ? 1 : 2) * SV_LTAB_QUADS * 64];  // per-wave entry stage
+  __shared__ sv_u4 s_stage[SV_BLOCK / 64][SV_LTAB_QUADS * 64];  // per-wave entry stage
   const uint32_t lane = threadIdx.x & 63u;
   sv_u4* stage = s_stage[threadIdx.x >> 6];
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -496,24 +479,11 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
   SV_UNROLL for (int i = 0; i < 10; ++i) o.v[i] = oc_from_hi(f.v[i]);
 }
 
-#ifndef SV_LAT_SPLIT
-#define SV_LAT_SPLIT 1
-#endif
-#ifndef SV_LAT_OWN
-#define SV_LAT_OWN 1
-#endif
-// 1: the base-point part [s]B of (*) (lattice.h) runs on wave 1 after its
-// table build (its own 112 doublings, 8 additions per half) while wave 0
-// runs the -A / -R chains without the 8 base additions per half; wave 0 adds
-// the result at the end (second LDS handoff).  Needs SV_LAT_SPLIT and
-// SV_LAT_OWN.
-#ifndef SV_LAT_BOFF
-#define SV_LAT_BOFF 1
-#endif
-// (in effect only with both prerequisites; the old-form loop keeps its base
-// additions, so the base part is never added twice)
-#define SV_LAT_BOFF_ON (SV_LAT_BOFF && SV_LAT_SPLIT && SV_LAT_OWN)
-#define SV_OCTET_BLOCK (SV_LAT_SPLIT ? 128 : 64)
+// Two waves per 8 signatures.  The base-point part [s]B of (*) (lattice.h)
+// runs on wave 1 after its table build (its own 112 doublings, 8 additions
+// per half) while wave 0 runs the -A / -R chains without base additions;
+// wave 0 adds the result at the end (second LDS handoff).
+#define SV_OCTET_BLOCK 128
 
 template <int MODE>
 __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams p) {
@@ -525,7 +495,6 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
   const uint64_t i = (uint64_t)blockIdx.x * SV_OSIGS + sl;
   const bool active = i < p.n;
   const uint64_t ii = active ? i : p.n - 1;  // idle tail octets redo the last item
-#if SV_LAT_SPLIT
   // Two waves per workgroup, same lane -> (signature, quad, role) map.  The
   // decompressions and table builds (wave 1) do not depend on the hash, the
   // scalar reduction and the Euclid reduction (wave 0), so the two chains run
@@ -541,41 +510,19 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     sv_unpack2(A, p.pk + 2 * ii);
     sv_unpack2(R, p.sig + 4 * ii);
   } else {
-#ifdef SV_QPROF_NOHASH  // (developer A/B builds only: phase timing of this kernel)
-    sv_unpack2(A, p.pk + 2 * ii);
-    sv_unpack2(S, p.sig + 4 * ii + 2);
-    SV_UNROLL for (int k = 0; k < 16; ++k) hram[k] = A[k & 7] ^ (uint32_t)k;
-#else
     sv_load_and_hash<MODE>(p, ii, A, S, hram);
-#endif
     sv_unpack2(R, p.sig + 4 * ii);
   }
   bool ok = true;
-#ifdef SV_QPROF_NODEC
-  if (dec_wave && false) {
-#else
   if (dec_wave) {
-#endif
-#else
-  uint32_t A[8], S[8], hram[16], R[8];
-  sv_load_and_hash<MODE>(p, ii, A, S, hram);
-  sv_unpack2(R, p.sig + 4 * ii);
-  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
-            sv_point_canonical(R);
-  {
-#endif
     // decompress: quad 0 -A, quad 1 -R; role 0 of each quad stores its table
     uint32_t E[8];
     SV_UNROLL for (int k = 0; k < 8; ++k) E[k] = half ? R[k] : A[k];
     ge_p3 Pt;
     const uint32_t dok = ge_frombytes(Pt, E, true) ? 1u : 0u;
-#if SV_LAT_SPLIT
     // (the DPP read outside the branch: a lane disabled by EXEC is no source)
     const uint32_t both = dok & oc_from_hi(dok);
     if (half == 0 && role == 0) s_dok[sl] = both;
-#else
-    ok = ok && (dok & oc_from_hi(dok)) != 0;  // (valid on quad 0, the lanes that use it)
-#endif
     ge_cached c1, ce;
     ge_p3_to_cached(c1, Pt);
     ge_cached_identity(ce);
@@ -595,14 +542,10 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
       if (store) sv_store_lentry((sv_u4*)(tab + e * SV_QENT_DW), ce);
     }
   }
-#if SV_LAT_SPLIT
-#if SV_LAT_BOFF_ON
   __shared__ int32_t s_bd[SV_OSIGS][2][SV_LB_DIGITS];  // base-point digits (wave 0 -> 1)
   __shared__ uint32_t s_pb[SV_OSIGS][SV_QENT_DW];       // [s]B, cached form (wave 1 -> 0)
-#endif
   if (dec_wave) {
     __syncthreads();  // tables and s_dok written; s_bd read below
-#if SV_LAT_BOFF_ON
     {
       // quad 0: [s_lo] B from e B, quad 1: [s_hi] 2^128 B from e 2^128 B;
       // digit j carries weight 2^(16 j) (Horner: 16 doublings between digits)
@@ -638,45 +581,31 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
       if (half == 0 && role == 0) sv_store_lentry((sv_u4*)&s_pb[sl][0], c1);
     }
     __syncthreads();  // s_pb written
-#endif
     return;
   }
   ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
        sv_point_canonical(R);
-#endif
   sv_lat lat;
   {
     uint32_t h[8];
     sc_reduce512(h, hram);
     sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
   }
-#ifdef SV_QPROF_NOMUL
-  const int W = 0;
-#else
   const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
-#endif
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
-#if SV_LAT_BOFF_ON
   if (role == 0) {
     SV_UNROLL for (int j = 0; j < SV_LB_DIGITS; ++j) s_bd[sl][half][j] = half ? D.dB1[j] : D.dB0[j];
   }
-#endif
   __syncthreads();  // tables visible to the whole quad
-#if SV_LAT_SPLIT
   ok = ok && s_dok[sl] != 0;
-#endif
 
-#if !SV_LAT_BOFF_ON
-  const sv_u4* btab = p.btab + (half ? SV_LBTAB_ENTRIES * SV_BTAB_QUADS : 0);
-#endif
   const uint32_t* tab = &s_tab[sl][half][0][0];
   // this quad's digit string and its top-digit carry
   uint32_t dg[8];
   SV_UNROLL for (int k = 0; k < 8; ++k) dg[k] = half ? D.dR[k] : D.dA[k];
   const bool top8 = half ? D.top8R : D.top8A;
   const bool flip = half && D.rneg;
-#if SV_LAT_OWN
   // own form (quad.h): lane r holds coordinate r of P until the end
   fe h;
   qo_identity(h, q);
@@ -684,17 +613,9 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     int32_t d = sc_pop_top(dg, 4);
     if (w == W - 1 && top8) d = 8;
     if (flip) d = -d;
-#if SV_LAT_BOFF_ON
     const bool bwin = false;  // (the base part runs on wave 1)
     const int32_t dB = 0;
     fe b;
-#else
-    int32_t dB0, dB1;
-    fe b;
-    const bool bwin = sv_lat_bdigits(D, w, dB0, dB1);
-    const int32_t dB = half ? dB1 : dB0;
-    if (bwin) qo_load_affine(b, btab + (dB < 0 ? -dB : dB) * SV_BTAB_QUADS, role, dB < 0);  // lands during the doublings
-#endif
     if (w != W - 1) {
       SV_NOUNROLL for (int k = 0; k < 4; ++k) qo_dbl(h, q);
     }
@@ -705,29 +626,6 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
   }
   ge_p3 P;
   qo_expand(P, h);
-#else
-  ge_p3 P;
-  fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
-  SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
-    int32_t d = sc_pop_top(dg, 4);
-    if (w == W - 1 && top8) d = 8;
-    if (flip) d = -d;
-    int32_t dB0, dB1;
-    fe b;
-    const bool bwin = sv_lat_bdigits(D, w, dB0, dB1);
-    const int32_t dB = half ? dB1 : dB0;
-    if (bwin) qd_load_affine(b, btab + (dB < 0 ? -dB : dB) * SV_BTAB_QUADS, role, dB < 0);  // lands during the doublings
-    if (w != W - 1) {
-      SV_NOUNROLL for (int k = 0; k < 4; ++k) qd_dbl(P, q, k == 3);
-    }
-    fe m;
-    qd_load_cached(m, tab + (d < 0 ? -d : d) * SV_QENT_DW, role, d < 0);
-    // T is needed after this addition by a base addition or, after the last
-    // window, by the final combination
-    qd_add(P, m, q, d < 0, bwin || w == 0);
-    if (bwin) qd_add(P, b, q, dB < 0, w == 0);
-  }
-#endif
   // quad 0: P_A + P_R, P_R in cached form from quad 1
   {
     ge_p3 PR;
@@ -741,14 +639,10 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     fe_add(ypx, PR.Y, PR.X);
     fe_sub(ymx, PR.Y, PR.X);
     fe_pick4(mine, q, t2d, PR.Z, ypx, ymx);  // role 0 2dT, 1 Z, 2 Y+X, 3 Y-X (qd_add's operand order)
-#if SV_LAT_BOFF_ON
     qd_add(P, mine, q, false, true);
     __syncthreads();  // [s]B from wave 1
     qd_load_cached(mine, &s_pb[sl][0], role, false);
     qd_add(P, mine, q, false, false);
-#else
-    qd_add(P, mine, q, false, false);
-#endif
   }
   ok = ok && sv_is_identity(P);
   const bool owner = half == 0 && role == 0;
@@ -767,15 +661,11 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
 
 __global__ __launch_bounds__(192) void sv_btab_init_kernel(uint32_t* btab) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-#if SV_LATTICE
   // table 0: e B (also the signer's table: it reads entries <= 2^(SV_B_BITS-1));
   // table 1: e 2^128 B
   if (e < SV_LBTAB_ENTRIES) sv_btab_entry_shift(btab + e * SV_BTAB_STRIDE, e, 0);
   else if (e < 2 * SV_LBTAB_ENTRIES)
     sv_btab_entry_shift(btab + e * SV_BTAB_STRIDE, e - SV_LBTAB_ENTRIES, 128);
-#else
-  if (e < SV_BTAB_ENTRIES) sv_btab_entry(btab + e * SV_BTAB_STRIDE, e);
-#endif
 }
 
 struct sv_sparams {
@@ -789,12 +679,7 @@ struct sv_sparams {
 };
 
 __global__ __launch_bounds__(SV_BLOCK, SV_WAVES_PER_SIMD) void sv_sign_kernel(sv_sparams p) {
-#if SV_B_BITS == 8
-  __shared__ sv_u4 s_btab[SV_BTAB_ENTRIES * (SV_BTAB_STRIDE / 4)];
-  sv_load_btab_lds(s_btab, p.btab);
-#else
   const sv_u4* s_btab = p.btab;
-#endif
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   sv_u4* slot = p.ws + gtid * SV_SLOT_QUADS;
@@ -920,11 +805,7 @@ static uint64_t sv_device_simds(void) {
 // Signatures per chunk for a throughput-path launch of n on the current
 // device (every chunk but the last has exactly this many; a multiple of 64,
 // at most SV_CHUNK).
-#ifndef SV_PLAN
-#define SV_PLAN 1  // 0: fixed SV_CHUNK-signature chunks (A/B baseline)
-#endif
 uint64_t sv_plan_chunk(uint64_t n, int share) {
-  if (!SV_PLAN) return SV_CHUNK;
   const uint64_t G = (n + 63) / 64;
   const uint64_t capG = SV_CHUNK / 64;
   const int mw = share ? sv_share_wps(sv_main_wps()) : sv_main_wps();
@@ -968,33 +849,17 @@ uint64_t sv_ws_cap(uint64_t n) {
 // digit records + window counts).  The latency kernel needs none.
 size_t sv_ws_bytes(unsigned grid, uint64_t cap) {
   size_t b = (size_t)grid * sv_ws_bytes_per_block();
-#if SV_LATTICE && SV_SPLIT
   const size_t s = (size_t)cap * (SV_SLOT_QUADS_L + SV_REC_QUADS) * sizeof(sv_u4) + (cap / 64) * 4;
   if (s > b) b = s;
-#else
-  (void)cap;
-#endif
   return b;
 }
 // workspace a verify launch of n signatures on `path` needs
 size_t sv_verify_ws_bytes(int path, unsigned grid, uint64_t n) {
-#if SV_LATTICE
   if (path == 2) return 0;
-#endif
-#if SV_LATTICE && SV_SPLIT
   (void)grid;
   return sv_ws_bytes(0, sv_ws_cap(n));
-#else
-  (void)n;
-  (void)path;
-  return sv_ws_bytes(grid, 0);
-#endif
 }
-#if SV_LATTICE
 #define SV_BTAB_TOTAL (2 * SV_LBTAB_ENTRIES)
-#else
-#define SV_BTAB_TOTAL SV_BTAB_ENTRIES
-#endif
 size_t sv_btab_bytes(void) { return (size_t)SV_BTAB_TOTAL * SV_BTAB_STRIDE * 4; }
 int sv_block_threads(void) { return SV_BLOCK; }
 
@@ -1005,16 +870,12 @@ hipError_t sv_launch_btab_init(uint32_t* d_btab, hipStream_t s) {
 
 int sv_occupancy_blocks_per_cu(void) {
   int b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-#if SV_LATTICE && SV_SPLIT
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b0, sv_main_kernel<false>, SV_BLOCK, 0) != hipSuccess) b0 = 1;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b3, sv_sign_kernel, SV_BLOCK, 0) != hipSuccess) b3 = 1;
   const int ms = b0 > b3 ? b0 : b3;
   (void)b1;
   (void)b2;
   return ms < 1 ? 1 : ms;
-#else
-#error "the product build is the split half-size path (SV_LATTICE = SV_SPLIT = 1)"
-#endif
 }
 
 size_t sv_key_table_entry_bytes(void) { return (size_t)SV_KT_QUADS * sizeof(sv_u4); }
@@ -1044,7 +905,6 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
   p.ws = (sv_u4*)ws;
   p.btab = (const sv_u4*)btab;
   p.dbg = dbg;
-#if SV_LATTICE
   if (path == 2) {  // SV_PATH_LATENCY
     const unsigned og = (unsigned)((n + SV_OSIGS - 1) / SV_OSIGS);
     if (mode == 0)
@@ -1055,9 +915,7 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
       hipLaunchKernelGGL(sv_octet_kernel<2>, dim3(og), dim3(SV_OCTET_BLOCK), 0, s, p);
     return hipGetLastError();
   }
-#endif
   (void)path;
-#if SV_LATTICE && SV_SPLIT
   const uint64_t cap = sv_ws_cap(n);
   const uint64_t chunk = sv_plan_chunk(n, share);
   const size_t plds = share ? sv_prep_share_lds() : 0;
@@ -1095,9 +953,6 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
       else hipLaunchKernelGGL(sv_main_kernel<false>, mg, dim3(SV_BLOCK), 0, s, c);
     }
   }
-#else
-#error "the product build is the split half-size path (SV_LATTICE = SV_SPLIT = 1)"
-#endif
   return hipGetLastError();
 }
 

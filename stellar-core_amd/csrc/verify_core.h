@@ -16,12 +16,12 @@
 //   64 windows of 4 bits.  Per window: 4 doublings; add table_A[d_A] with
 //   d_A in [-8, 8] (signed radix 16 of h); on every 4th window also add
 //   table_B[d_B], d_B in [-2^15, 2^15] (signed radix 2^16 of S; SV_B_BITS).
-//   table_A = {0..8}·(-A) in cached form, built per lane into an HBM workspace
-//   slot (1584 B/lane, lane-major so a lane's entry is 176 contiguous bytes;
-//   too big for LDS at >= 2 waves/SIMD); each window's table_A and table_B
-//   entries are prefetched into LDS by DMA while the window doubles;
-//   table_B = {0..2^15}·B in affine precomp form, one global copy per device.
-//   Zero digits add the identity entry, so every lane does identical work.
+//   table_A = {0..8}·(-A) in cached form, built per lane into a workspace
+//   slot; table_B = {0..2^15}·B in affine precomp form, one global copy per
+//   device.  Zero digits add the identity entry, so every lane does
+//   identical work.  This full-length form (sv_double_scalarmult) serves the
+//   signer and host builds; the verify kernels evaluate the half-size
+//   equation of lattice.h (sv_lat_* below, sv_kernels.hip, sv_comb.hip).
 #pragma once
 
 #include "ge25519.h"
@@ -35,15 +35,10 @@ struct __attribute__((aligned(16))) sv_u4 {
 
 // Every table field element is padded to 12 dwords (3 quads) so a negative
 // digit's (Y+X) <-> (Y-X) swap is an address choice at load time.
-// B-table: entry e = e·B as 36 dwords: ypx[12] ymx[12] xy2d[12].
-//   SV_B_BITS 16 (default): signed radix-2^16 digits of S, one B addition
-//     every 4th window (16 per signature), 2^15 + 1 entries = 4.7 MB read from
-//     global memory (L2/MALL-resident).
-//   SV_B_BITS 8: signed radix-256 digits, every other window (32 additions),
-//     129 entries = 18.6 KB staged into LDS per workgroup.
-#ifndef SV_B_BITS
+// B-table: entry e = e·B as 36 dwords: ypx[12] ymx[12] xy2d[12].  Signed
+// radix-2^16 digits of S, one B addition every 4th window (16 per signature),
+// 2^15 + 1 entries = 4.7 MB read from global memory (L2/MALL-resident).
 #define SV_B_BITS 16
-#endif
 #define SV_BTAB_ENTRIES ((1 << (SV_B_BITS - 1)) + 1)
 #define SV_BTAB_STRIDE 36
 #define SV_BTAB_DWORDS (SV_BTAB_ENTRIES * SV_BTAB_STRIDE)
@@ -139,20 +134,13 @@ SV_COLD void sv_build_atab(sv_u4* slot, int qstride, const ge_p3& negA) {
   }
 }
 
-// Builds table_A for -A in the lane's workspace slot and computes the
-// projective point Rp = [h](-A) + [S]B  (step (7)).
-//
-// Step machine: per window w (64 of them, MSB first) run steps
-//   s = 0..3  doubling, s = 4  add table_A[d_A], s = 5 (even w) add table_B[d_B]
-// with one code instance of each step kind; every branch is wave-uniform.
-// Per-wave LDS stage: the window's table_A entry [11 quads][64 lanes] x 16 B,
-// then (SV_STAGE_B) its table_B entry [9 quads][64 lanes] -- 20 KiB per wave,
-// so two 256-thread workgroups fill the CU's 160 KiB.
-#ifndef SV_STAGE_B
-#define SV_STAGE_B (SV_B_BITS == 16)  // (an LDS-resident radix-256 table needs no stage)
-#endif
+// Computes the projective point [h](-A) + [S]B with table_A of -A built in the
+// lane's workspace slot: 64 windows (MSB first), per window 4 doublings, an
+// addition of table_A[d_A] and, every 4th window, of table_B[d_B] (signed
+// radix-2^16 digits of S).  Used by the signer (h = 0: only the identity entry
+// of table_A is read) and by host builds; the verify kernels run the
+// half-size equation (sv_main_scalarmult, the octet and comb kernels).
 #define SV_BTAB_QUADS (SV_BTAB_STRIDE / 4)
-#define SV_STAGE_QUADS ((SV_ATAB_QUADS + (SV_STAGE_B ? SV_BTAB_QUADS : 0)) * 64)
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // LDS-DMA of quad Q of an entry at per-lane address SRC + 16*OFF bytes into
@@ -166,26 +154,9 @@ SV_COLD void sv_build_atab(sv_u4* slot, int qstride, const ge_p3& negA) {
   __builtin_amdgcn_global_load_lds(                                                                   \
       (const void*)(SRC),                                                                             \
       (__attribute__((address_space(3))) void*)((char*)((STAGE) + (ROW) * 64) - 16 * (OFF)), 16, 16 * (OFF), 0)
-// Device: the window's table_A entry is fetched by LDS-DMA (global_load_lds,
-// no VGPR destination) when the window starts, so the HBM/L2 latency hides
-// behind the window's 4 doublings instead of stalling the addition.  The
-// +/- swap of (Y+X, Y-X) is done by the per-lane SOURCE address; the LDS image
-// is lane-linear (a DMA writes wave-uniform base + lane x 16 B).
-SV_HD void sv_stage_aentry(sv_u4* stage, const sv_u4* slot, int qstride, int32_t d) {
-  const bool neg = d < 0;
-  const sv_u4* e = slot + (neg ? -d : d) * SV_ATAB_QUADS * qstride;
-  const sv_u4* ea = e + (neg ? 3 : 0) * qstride;
-  const sv_u4* eb = e + (neg ? 0 : 3) * qstride;
-  // the previous window's LDS reads of the stage have retired before the
-  // DMA may overwrite it
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  SV_UNROLL for (int q = 0; q < SV_ATAB_QUADS; ++q) {
-    const sv_u4* src = q < 3 ? ea + q * qstride : (q < 6 ? eb + (q - 3) * qstride : e + q * qstride);
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(stage + q * 64),
-                                     16, 0, 0);
-  }
-}
-// Same for the window's table_B entry (4.7 MB global table, L2/MALL-hot).
+// A base-point table entry (affine: y+x, y-x, 2dxy; 4.7 MB tables, L2 /
+// Infinity-Cache-hot) into a lane-linear LDS stage, the +/- swap of (y+x, y-x)
+// done by the per-lane source address.
 SV_HD void sv_stage_bentry(sv_u4* stageB, const sv_u4* btab, int32_t d) {
   const bool neg = d < 0;
   const sv_u4* e = btab + (neg ? -d : d) * SV_BTAB_QUADS;
@@ -197,27 +168,14 @@ SV_HD void sv_stage_bentry(sv_u4* stageB, const sv_u4* btab, int32_t d) {
   SV_GLDS(e, 6, stageB, 6); SV_GLDS(e, 7, stageB, 7); SV_GLDS(e, 8, stageB, 8);
   static_assert(SV_BTAB_QUADS == 9, "entry size");
 }
-// hipcc does not count LDS-DMA completion before LDS reads: wait explicitly
-// (no other vector-memory op is in flight inside the window).
-SV_HD void sv_stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 #endif
 
-// STAGED (device only): table_A entries arrive through the wave's LDS stage.
-template <bool STAGED = false>
 SV_HD void sv_double_scalarmult(ge_p3& P, const ge_p3& negA, const uint32_t h[8], const uint32_t S[8],
-                                sv_u4* slot, int qstride, const sv_u4* btab, sv_u4* stage = nullptr) {
+                                sv_u4* slot, int qstride, const sv_u4* btab) {
   sv_build_atab(slot, qstride, negA);
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (STAGED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // table stores before the DMA reads
-#endif
-
   uint32_t da[8], db[8];
   sc_digits_r16(da, h);
-#if SV_B_BITS == 16
   sc_digits_r65536(db, S);
-#else
-  sc_digits_r256(db, S);
-#endif
 
   fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
   ge_p1p1 Q;
@@ -225,57 +183,26 @@ SV_HD void sv_double_scalarmult(ge_p3& P, const ge_p3& negA, const uint32_t h[8]
     const int nsteps = (w & (SV_B_BITS / 4 - 1)) ? 5 : 6;
     const int32_t dA = sc_pop_top(da, 4);
     const int32_t dB = nsteps == 6 ? sc_pop_top(db, SV_B_BITS) : 0;
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (STAGED) {
-      sv_stage_aentry(stage, slot, qstride, dA);
-      if (SV_STAGE_B && nsteps == 6) sv_stage_bentry(stage + SV_ATAB_QUADS * 64, btab, dB);
-    }
-#endif
     SV_NOUNROLL for (int s = 0; s < nsteps; ++s) {
       if (s < 4) {
         ge_dbl(Q, P.X, P.Y, P.Z);
       } else {
-        // (loading the table_A entry into VGPRs before the doublings spills:
-        // a doubling leaves no room for 40 more live VGPRs at 2 waves/SIMD;
-        // the staged path parks it in LDS instead)
         fe qa, qb, qz, qt;
         bool neg;
         const bool zone = s == 5;
         if (!zone) {
           neg = dA < 0;
-#if defined(__HIP_DEVICE_COMPILE__)
-          if (STAGED) {
-            sv_stage_wait();
-            const sv_u4* st = stage + __lane_id();
-            sv_load_fe3(qa, st, 64);
-            sv_load_fe3(qb, st + 3 * 64, 64);
-            sv_load_fe_pair(qz, qt, st + 6 * 64, 64);
-          } else
-#endif
-          {
-            const sv_u4* e = slot + (neg ? -dA : dA) * SV_ATAB_QUADS * qstride;
-            sv_load_fe3(qa, e + (neg ? 3 : 0) * qstride, qstride);
-            sv_load_fe3(qb, e + (neg ? 0 : 3) * qstride, qstride);
-            sv_load_fe_pair(qz, qt, e + 6 * qstride, qstride);
-          }
+          const sv_u4* e = slot + (neg ? -dA : dA) * SV_ATAB_QUADS * qstride;
+          sv_load_fe3(qa, e + (neg ? 3 : 0) * qstride, qstride);
+          sv_load_fe3(qb, e + (neg ? 0 : 3) * qstride, qstride);
+          sv_load_fe_pair(qz, qt, e + 6 * qstride, qstride);
         } else {
           neg = dB < 0;
           fe_1(qz);
-#if defined(__HIP_DEVICE_COMPILE__)
-          if (STAGED && SV_STAGE_B) {
-            sv_stage_wait();
-            const sv_u4* st = stage + SV_ATAB_QUADS * 64 + __lane_id();
-            sv_load_fe3(qa, st, 64);
-            sv_load_fe3(qb, st + 3 * 64, 64);
-            sv_load_fe3(qt, st + 6 * 64, 64);
-          } else
-#endif
-          {
-            const sv_u4* e = btab + (neg ? -dB : dB) * SV_BTAB_QUADS;
-            sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
-            sv_load_fe3(qb, e + (neg ? 0 : 3), 1);
-            sv_load_fe3(qt, e + 6, 1);
-          }
+          const sv_u4* e = btab + (neg ? -dB : dB) * SV_BTAB_QUADS;
+          sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
+          sv_load_fe3(qb, e + (neg ? 0 : 3), 1);
+          sv_load_fe3(qt, e + 6, 1);
         }
         ge_add_preswapped(Q, P, qa, qb, qz, qt, neg, zone);
       }
@@ -297,10 +224,8 @@ SV_HD void sv_double_scalarmult_encode(uint32_t enc[8], const ge_p3& negA, const
 // lane rejected by (1)-(5), P.Z is set to 1 so that a batch inversion over
 // several signatures (sv_finalize_batch) can never be poisoned by a garbage
 // point; its encoding is irrelevant to its (already false) verdict.
-template <bool STAGED = false>
 SV_HD bool sv_verify_pre(ge_p3& P, const uint32_t A[8], const sv_u4* Rp, const uint32_t S[8],
-                         const uint32_t hram[16], sv_u4* slot, int qstride, const sv_u4* btab,
-                         sv_u4* stage = nullptr) {
+                         const uint32_t hram[16], sv_u4* slot, int qstride, const sv_u4* btab) {
   bool ok;
   {
     uint32_t R[8];
@@ -319,7 +244,7 @@ SV_HD bool sv_verify_pre(ge_p3& P, const uint32_t A[8], const sv_u4* Rp, const u
   uint32_t Sc[8];
   SV_UNROLL for (int i = 0; i < 8; ++i) Sc[i] = S[i];
   Sc[7] &= 0x1fffffffu;
-  sv_double_scalarmult<STAGED>(P, negA, h, Sc, slot, qstride, btab, stage);
+  sv_double_scalarmult(P, negA, h, Sc, slot, qstride, btab);
   if (!ok) fe_1(P.Z);
   return ok;
 }
@@ -541,10 +466,7 @@ SV_HD void sv_load_lentry(fe& qa, fe& qb, fe& qz, fe& qt, const sv_u4* p, int qs
 
 // {0..8}·P in cached form into tab (9 entries x 10 quads, lane-contiguous).
 // P comes straight from ge_frombytes, so it is affine (Z = 1): each step adds
-// it with the mixed law (2 Z1 Z2 = 2 Z1, no product; SV_LTAB_MADD).
-#ifndef SV_LTAB_MADD
-#define SV_LTAB_MADD 1
-#endif
+// it with the mixed law (2 Z1 Z2 = 2 Z1, no product).
 SV_COLD void sv_build_ltab(sv_u4* tab, const ge_p3& P) {
   ge_cached c1, ce;
   ge_p3_to_cached(c1, P);
@@ -554,7 +476,7 @@ SV_COLD void sv_build_ltab(sv_u4* tab, const ge_p3& P) {
   ge_p3 P3 = P;
   ge_p1p1 Q;
   SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
-    ge_add_preswapped(Q, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, SV_LTAB_MADD != 0);
+    ge_add_preswapped(Q, P3, c1.YpX, c1.YmX, c1.Z, c1.T2d, false, true);
     ge_p1p1_to_p3(P3, Q);
     ge_p3_to_cached(ce, P3);
     sv_store_lentry(tab + e * SV_LTAB_QUADS, ce);
@@ -633,18 +555,10 @@ SV_COLD void sv_lat_prepare(sv_lat_digits& D, const sv_lat& lat, const uint32_t 
   sc_digits_lb(D.dB0, D.dB1, s);  // s < L: low / high 128-bit halves, one carry chain
 }
 
-// 1: one 10-quad stage region per wave instead of two (10 KB): each entry is
-// DMA'd when the previous addition's entry has been read, so its latency hides
-// behind one addition instead of the window's doublings; frees LDS for more
-// waves per CU.
-#ifndef SV_STAGE_ONE
-#define SV_STAGE_ONE 1
-#endif
-// 1: the window's two base-point entries are also staged by LDS-DMA (into the
-// A and R regions once those entries have been read)
-#ifndef SV_LAT_STAGE_B
-#define SV_LAT_STAGE_B 1
-#endif
+// The main kernel's entry stage: ONE 10-quad region per wave (10 KB); each
+// entry is DMA'd when the previous addition's entry has been read, so its
+// latency hides behind one addition (sv_main_scalarmult), and LDS is left for
+// more waves per CU.
 #if defined(__HIP_DEVICE_COMPILE__)
 // one lane-contiguous 10-quad table entry into a lane-linear stage
 SV_HD void sv_stage_lentry(sv_u4* stage, const sv_u4* entry) {
@@ -661,11 +575,10 @@ SV_HD void sv_stage_lentry(sv_u4* stage, const sv_u4* entry) {
 // Step machine per window w: s = 0..3 doubling (skipped in the top window,
 // where P is the identity), s = 4 add tabA[dA], s = 5 add tabR[+-dR], and on
 // windows w = 4j, j < SV_LB_DIGITS: s = 6 add btab0[dB0_j], s = 7 add btab1[dB1_j].
-// STAGED (device): the window's A and R entries are DMA'd into the wave's LDS
-// stage (2 x 10 quads x 64 lanes) when the window starts.
-template <bool STAGED = false>
+// The host form (the CPU path, sv_cpu.cpp); the main kernel runs the same
+// step machine with its entries staged by LDS-DMA (sv_main_scalarmult).
 SV_HD void sv_lat_scalarmult(ge_p3& P, sv_lat_digits& D, int W, const sv_u4* tabA, const sv_u4* tabR,
-                             const sv_u4* btab0, const sv_u4* btab1, sv_u4* stage = nullptr) {
+                             const sv_u4* btab0, const sv_u4* btab1) {
   fe_0(P.X); fe_1(P.Y); fe_1(P.Z); fe_0(P.T);
   ge_p1p1 Q;
   SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
@@ -680,15 +593,6 @@ SV_HD void sv_lat_scalarmult(ge_p3& P, sv_lat_digits& D, int W, const sv_u4* tab
     const bool bwin = sv_lat_bdigits(D, w, dB0, dB1);
     const int nsteps = bwin ? 8 : 6;
     const int s0 = (w == W - 1) ? 4 : 0;
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (STAGED) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      sv_stage_lentry(stage, tabA + (dA < 0 ? -dA : dA) * SV_LTAB_QUADS);
-#if !SV_STAGE_ONE
-      sv_stage_lentry(stage + SV_LTAB_QUADS * 64, tabR + (dR < 0 ? -dR : dR) * SV_LTAB_QUADS);
-#endif
-    }
-#endif
     SV_NOUNROLL for (int s = s0; s < nsteps; ++s) {
       if (s < 4) {
         ge_dbl(Q, P.X, P.Y, P.Z);
@@ -699,66 +603,16 @@ SV_HD void sv_lat_scalarmult(ge_p3& P, sv_lat_digits& D, int W, const sv_u4* tab
         if (!zone) {
           const int32_t d = s == 4 ? dA : dR;
           neg = d < 0;
-#if defined(__HIP_DEVICE_COMPILE__)
-          if (STAGED && SV_STAGE_ONE) {
-            // one region: the entry DMA'd for this step has landed; once it is
-            // read, the region receives the next addition's entry
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            sv_load_lentry(qa, qb, qz, qt, stage + __lane_id(), 64, neg);
-            if (s == 4 || bwin) {
-              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-              if (s == 4) sv_stage_lentry(stage, tabR + (dR < 0 ? -dR : dR) * SV_LTAB_QUADS);
-              else sv_stage_bentry(stage, btab0, dB0);
-            }
-          } else if (STAGED) {
-            // s = 4: the A and R entries (DMA'd at window start) have landed
-            if (s == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            sv_u4* reg = stage + (s == 4 ? 0 : SV_LTAB_QUADS * 64);
-            sv_load_lentry(qa, qb, qz, qt, reg + __lane_id(), 64, neg);
-            if (SV_LAT_STAGE_B && bwin) {
-              // this region is free once its reads retire: stage the B entry
-              // that step s + 2 adds (B0 into A's region, B1 into R's)
-              const int32_t db = s == 4 ? dB0 : dB1;
-              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-              sv_stage_bentry(reg, s == 4 ? btab0 : btab1, db);
-            }
-          } else
-#endif
-          {
-            const sv_u4* e = (s == 4 ? tabA : tabR) + (neg ? -d : d) * SV_LTAB_QUADS;
-            sv_load_lentry(qa, qb, qz, qt, e, 1, neg);
-          }
+          const sv_u4* e = (s == 4 ? tabA : tabR) + (neg ? -d : d) * SV_LTAB_QUADS;
+          sv_load_lentry(qa, qb, qz, qt, e, 1, neg);
         } else {
           const int32_t d = s == 6 ? dB0 : dB1;
           neg = d < 0;
           fe_1(qz);
-#if defined(__HIP_DEVICE_COMPILE__)
-          if (STAGED && SV_STAGE_ONE) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const sv_u4* st = stage + __lane_id();
-            sv_load_fe3(qa, st, 64);
-            sv_load_fe3(qb, st + 3 * 64, 64);
-            sv_load_fe3(qt, st + 6 * 64, 64);
-            if (s == 6) {
-              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-              sv_stage_bentry(stage, btab1, dB1);
-            }
-          } else if (STAGED && SV_LAT_STAGE_B) {
-            // B0's DMA is older than B1's 9: vmcnt(9) covers it
-            if (s == 6) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const sv_u4* st = stage + (s == 6 ? 0 : SV_LTAB_QUADS * 64) + __lane_id();
-            sv_load_fe3(qa, st, 64);
-            sv_load_fe3(qb, st + 3 * 64, 64);
-            sv_load_fe3(qt, st + 6 * 64, 64);
-          } else
-#endif
-          {
-            const sv_u4* e = (s == 6 ? btab0 : btab1) + (neg ? -d : d) * SV_BTAB_QUADS;
-            sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
-            sv_load_fe3(qb, e + (neg ? 0 : 3), 1);
-            sv_load_fe3(qt, e + 6, 1);
-          }
+          const sv_u4* e = (s == 6 ? btab0 : btab1) + (neg ? -d : d) * SV_BTAB_QUADS;
+          sv_load_fe3(qa, e + (neg ? 3 : 0), 1);
+          sv_load_fe3(qb, e + (neg ? 0 : 3), 1);
+          sv_load_fe3(qt, e + 6, 1);
         }
         ge_add_preswapped(Q, P, qa, qb, qz, qt, neg, zone);
       }
@@ -777,39 +631,15 @@ SV_HD bool sv_is_identity(const ge_p3& P) {
 // Steps (1)-(5) of libsodium plus the decode of R (lattice.h), the Euclid
 // reduction and the table build.  Returns the pre-verdict and the lane's
 // window count in *W_lane; the caller picks the wave's W >= every W_lane.
-#ifndef SV_PREP_SEQ
-#define SV_PREP_SEQ 1
-#endif
-// a_status >= 0 (SV_PREP_SEQ 1): A's checks and decode are already known --
+// a_status >= 0: A's checks and decode are already known --
 // a_status != 0 iff A is canonical, not of small order and decodes (the
 // per-key tables of the throughput path, sv_kernels.hip) -- and table_A is
 // not built (the caller reads the key's cached table instead).
 SV_COLD bool sv_lat_pre(sv_lat& lat, const uint32_t A[8], const uint32_t R[8], const uint32_t S[8],
                         const uint32_t hram[16], sv_u4* tabA, sv_u4* tabR, bool trivial = false,
                         int a_status = -1) {
-#if SV_PREP_SEQ == 1
   bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(R) &&
             (a_status >= 0 ? a_status != 0 : (sv_point_canonical(A) && !sv_small_order(A)));
-#else
-  // (the A/B variants always decode A: a cached table, if any, holds the same entries)
-  a_status = -1;
-  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
-            sv_point_canonical(R);
-#endif
-#if SV_PREP_SEQ == 2
-  // as below, with A and R through ONE copy of the decode + table code (a
-  // rolled loop: the inlined exponentiation chain is ~30 KB of code per copy)
-  uint32_t h[8];
-  sc_reduce512(h, hram);
-  SV_NOUNROLL for (int k = 0; k < 2; ++k) {
-    uint32_t w[8];
-    SV_UNROLL for (int i = 0; i < 8; ++i) w[i] = k ? R[i] : A[i];
-    ge_p3 negP;
-    ok = ge_frombytes(negP, w, true) && ok;
-    sv_build_ltab(k ? tabR : tabA, negP);
-  }
-  sc_lattice_reduce(lat, h, trivial);
-#elif SV_PREP_SEQ
   // one point live at a time: h first (hram dies), then decode + table of -A,
   // of -R, then the Euclid reduction with no point live
   uint32_t h[8];
@@ -825,15 +655,5 @@ SV_COLD bool sv_lat_pre(sv_lat& lat, const uint32_t A[8], const uint32_t R[8], c
     sv_build_ltab(tabR, negR);
   }
   sc_lattice_reduce(lat, h, trivial);
-#else
-  ge_p3 negA, negR;
-  ok = ge_frombytes(negA, A, true) && ok;
-  ok = ge_frombytes(negR, R, true) && ok;
-  uint32_t h[8];
-  sc_reduce512(h, hram);
-  sc_lattice_reduce(lat, h, trivial);
-  sv_build_ltab(tabA, negA);
-  sv_build_ltab(tabR, negR);
-#endif
   return ok;
 }

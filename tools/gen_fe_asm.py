@@ -188,7 +188,7 @@ def gen_sq(dbl):
 def main():
     print("// GENERATED by tools/gen_fe_asm.py -- do not edit.  Device-only field")
     print("// products as single inline-asm statements (see the generator's docstring);")
-    print("// included by fe25519.h under SV_FE_ASM.  Same arithmetic and bounds as")
+    print("// included by fe25519.h for device builds.  Same arithmetic and bounds as")
     print("// fe_mul_cm / fe_sq_cm there, which the host build and tests/ exercise.")
     print("#pragma once")
     print()
