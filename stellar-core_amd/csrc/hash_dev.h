@@ -72,7 +72,7 @@ SV_HD void blake2b_compress(uint64_t h[8], const uint64_t m[16], uint64_t t, boo
     SV_B2G(3, 4, 9, 14, m[SIG[r][14]], m[SIG[r][15]]);
   }
 #undef SV_B2G
-  SV_UNROLL for (int i = 0; i < 8; ++i) h[i] ^= v[i] ^ v[i + 8];
+  SV_UNROLL for (int i = 0; i < 8; ++i) h[i] = sv_xor3_64(h[i], v[i], v[i + 8]);
 }
 
 // Verify-cache key: BLAKE2b-256 of pk(32) || sig(64) || msg(len), as 8 LE words.
@@ -126,15 +126,15 @@ SV_HD void sha256_compress(uint32_t st[8], uint32_t w[16]) {
     SV_UNROLL for (int i = 0; i < 16; ++i) {
       if (pass > 0) {
         const uint32_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-        const uint32_t s0 = sv_rotr32(w15, 7) ^ sv_rotr32(w15, 18) ^ (w15 >> 3);
-        const uint32_t s1 = sv_rotr32(w2, 17) ^ sv_rotr32(w2, 19) ^ (w2 >> 10);
+        const uint32_t s0 = sv_xor3_32(sv_rotr32(w15, 7), sv_rotr32(w15, 18), w15 >> 3);
+        const uint32_t s1 = sv_xor3_32(sv_rotr32(w2, 17), sv_rotr32(w2, 19), w2 >> 10);
         w[i] += s0 + w[(i + 9) & 15] + s1;
       }
-      const uint32_t S1 = sv_rotr32(e, 6) ^ sv_rotr32(e, 11) ^ sv_rotr32(e, 25);
+      const uint32_t S1 = sv_xor3_32(sv_rotr32(e, 6), sv_rotr32(e, 11), sv_rotr32(e, 25));
       const uint32_t ch = (e & f) ^ (~e & g);
       const uint32_t t1 = h + S1 + ch + SV_SHA256_K[pass * 16 + i] + w[i];
-      const uint32_t S0 = sv_rotr32(a, 2) ^ sv_rotr32(a, 13) ^ sv_rotr32(a, 22);
-      const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+      const uint32_t S0 = sv_xor3_32(sv_rotr32(a, 2), sv_rotr32(a, 13), sv_rotr32(a, 22));
+      const uint32_t mj = sv_maj32(a, b, c);
       h = g; g = f; f = e; e = d + t1;
       d = c; c = b; b = a; a = t1 + S0 + mj;
     }

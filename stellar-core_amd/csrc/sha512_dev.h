@@ -53,20 +53,6 @@ SV_HD uint64_t sv_rotr64(uint64_t x, int n) {
   return (x >> n) | (x << (64 - n));
 #endif
 }
-// maj(a, b, c) = bfi(a ^ b, c, b): where a and b differ c decides.  LLVM
-// canonicalises every C spelling of this back to and/or/xor (4 ops per half),
-// so the device form is one v_bfi_b32 per half.
-SV_HD uint64_t sv_maj64(uint64_t a, uint64_t b, uint64_t c) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint64_t x = a ^ b;
-  uint32_t lo, hi;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(lo) : "v"((uint32_t)x), "v"((uint32_t)c), "v"((uint32_t)b));
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(x >> 32)), "v"((uint32_t)(c >> 32)), "v"((uint32_t)(b >> 32)));
-  return ((uint64_t)hi << 32) | lo;
-#else
-  return (a & b) ^ (c & (a ^ b));
-#endif
-}
 SV_HD uint32_t sv_bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }
@@ -89,10 +75,10 @@ SV_HD void sha512_init(uint64_t st[8]) {
 // unrolled rounds (static register indices, uniform round-constant loads).
 #define SV_SHA512_ROUND(Wi, Ki)                                                       \
   do {                                                                               \
-    const uint64_t S1 = sv_rotr64(e, 14) ^ sv_rotr64(e, 18) ^ sv_rotr64(e, 41);       \
+    const uint64_t S1 = sv_xor3_64(sv_rotr64(e, 14), sv_rotr64(e, 18), sv_rotr64(e, 41)); \
     const uint64_t ch = (e & f) ^ (~e & g);                                           \
     const uint64_t t1 = h + S1 + ch + (Ki) + (Wi);                                    \
-    const uint64_t S0 = sv_rotr64(a, 28) ^ sv_rotr64(a, 34) ^ sv_rotr64(a, 39);       \
+    const uint64_t S0 = sv_xor3_64(sv_rotr64(a, 28), sv_rotr64(a, 34), sv_rotr64(a, 39)); \
     const uint64_t mj = sv_maj64(a, b, c);                                            \
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;           \
   } while (0)
@@ -102,8 +88,8 @@ SV_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   SV_NOUNROLL for (int pass = 1; pass < 5; ++pass) {
     SV_UNROLL for (int i = 0; i < 16; ++i) {
       const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-      const uint64_t s0 = sv_rotr64(w15, 1) ^ sv_rotr64(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = sv_rotr64(w2, 19) ^ sv_rotr64(w2, 61) ^ (w2 >> 6);
+      const uint64_t s0 = sv_xor3_64(sv_rotr64(w15, 1), sv_rotr64(w15, 8), w15 >> 7);
+      const uint64_t s1 = sv_xor3_64(sv_rotr64(w2, 19), sv_rotr64(w2, 61), w2 >> 6);
       w[i] = w[i] + s0 + w[(i + 9) & 15] + s1;
       SV_SHA512_ROUND(w[i], SV_SHA512_K[16 * pass + i]);
     }

@@ -43,3 +43,41 @@
 #define SV_UNROLL _Pragma("GCC unroll 64")
 #define SV_NOUNROLL _Pragma("GCC unroll 1")
 #endif
+
+// Three-input bit functions as gfx950's v_bitop3_b32 (any function of three
+// inputs by its 8-entry truth table, one VALU op per 32-bit half): xor3 (0x96,
+// the Sigma / sigma functions) and maj (0xE8).  LLVM emits two v_xor_b32 for
+// a ^ b ^ c and canonicalises every C spelling of maj to and/or/xor; the
+// truth tables of both are symmetric in the operands.
+SV_HD uint64_t sv_xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x96);
+  return ((uint64_t)hi << 32) | lo;
+#else
+  return a ^ b ^ c;
+#endif
+}
+SV_HD uint32_t sv_xor3_32(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+SV_HD uint64_t sv_maj64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xE8);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xE8);
+  return ((uint64_t)hi << 32) | lo;
+#else
+  return (a & b) ^ (c & (a ^ b));
+#endif
+}
+SV_HD uint32_t sv_maj32(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+#else
+  return (a & b) ^ (c & (a ^ b));
+#endif
+}
