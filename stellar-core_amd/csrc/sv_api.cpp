@@ -43,7 +43,6 @@
 #include <functional>
 #include <mutex>
 #include <random>
-#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -1579,7 +1578,40 @@ void shutdown_locked() {
 // :317-330, one mutex).  A thread takes it once however deep its entry points
 // nest: re-acquiring a shared lock behind a queued writer would deadlock.
 // Lock order: g_life, then g_mu, then a slot's lat.mu, then its mu.
-std::shared_mutex g_life;
+// Writer-preferring: once a teardown waits, new calls queue behind it (glibc's
+// rwlock, behind std::shared_mutex, prefers readers, so callers that keep a
+// slot busy back to back would starve sv_set_device_map forever).
+class LifeLock {
+ public:
+  void lock_shared() {
+    std::unique_lock<std::mutex> l(m_);
+    cv_.wait(l, [&] { return !writer_ && waiting_ == 0; });
+    ++readers_;
+  }
+  void unlock_shared() {
+    std::lock_guard<std::mutex> l(m_);
+    if (--readers_ == 0 && waiting_ != 0) cv_.notify_all();
+  }
+  void lock() {
+    std::unique_lock<std::mutex> l(m_);
+    ++waiting_;
+    cv_.wait(l, [&] { return !writer_ && readers_ == 0; });
+    --waiting_;
+    writer_ = true;
+  }
+  void unlock() {
+    std::lock_guard<std::mutex> l(m_);
+    writer_ = false;
+    cv_.notify_all();
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  int readers_ = 0, waiting_ = 0;
+  bool writer_ = false;
+};
+LifeLock g_life;
 thread_local int t_life_depth = 0;
 struct LifeGuard {
   LifeGuard() {
@@ -1605,7 +1637,7 @@ int sv_init(void) { return ensure_init(); }
 
 void sv_shutdown(void) {
   if (t_life_depth != 0) return;  // (from inside an engine call, e.g. a keys-ready callback: refused)
-  std::unique_lock<std::shared_mutex> life(g_life);  // waits for every in-flight call
+  std::unique_lock<LifeLock> life(g_life);  // waits for every in-flight call
   std::lock_guard<std::mutex> g(g_mu);
   shutdown_locked();
 }
@@ -1616,7 +1648,7 @@ int sv_set_device_map(const int* physical, int count) {
   // teardown and the new map in ONE critical section: a concurrent first use
   // cannot re-initialise with the old map in between; in-flight calls finish
   // first (g_life)
-  std::unique_lock<std::shared_mutex> life(g_life);
+  std::unique_lock<LifeLock> life(g_life);
   std::lock_guard<std::mutex> g(g_mu);
   shutdown_locked();
   g_map.assign(physical, physical + count);

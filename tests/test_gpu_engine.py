@@ -382,12 +382,14 @@ def test_remap_and_shutdown_under_concurrent_calls(sv, dev, golden):
     tpk, tsig, tm = random_dataset(sv, dev, 20000, 91)
     stop = threading.Event()
     errors, counts = [], [0] * 4
+    import time
+    deadline = time.monotonic() + 90  # (a deadlock fails the test instead of hanging the suite)
 
     def worker(k):
         st = torch.cuda.Stream(dev)
         tv = torch.zeros(20000, dtype=torch.uint8, device=dev)
         try:
-            while not stop.is_set():
+            while not stop.is_set() and time.monotonic() < deadline:
                 if k == 3:
                     with torch.cuda.stream(st):
                         sv.verify_device(0, tpk.data_ptr(), tsig.data_ptr(), tm.data_ptr(), 20000, tv.data_ptr(),

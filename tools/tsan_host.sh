@@ -8,17 +8,24 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 O=/tmp/tsan
 mkdir -p $O
 cd "$R/stellar-core_amd"
+# clang's ThreadSanitizer (ROCm's LLVM): GCC 11's libtsan has no
+# pthread_cond_clockwait interceptor, which libstdc++'s condition_variable::
+# wait_for uses, so it loses track of the mutex a timed wait releases and
+# reports the next lock of it as a double lock (false positives in the
+# micro-batcher's deadline waits, seen on round-3 and round-4 sources alike)
+CXX=/opt/rocm/lib/llvm/bin/clang++
+TSAN_RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.tsan-x86_64.so | head -1)
 for f in hashes PubKeyUtils SignatureChecker VerifyMicroBatcher TransactionSignatures host_capi; do
-  g++ -O1 -g -std=c++17 -fPIC -fsanitize=thread -c csrc/host/$f.cpp -o $O/$f.o
+  $CXX -O1 -g -std=c++17 -fPIC -fsanitize=thread -c csrc/host/$f.cpp -o $O/$f.o
 done
-g++ -shared -fsanitize=thread -o $O/libstellar_host.so $O/*.o -L. -lstellar_sigverify \
+$CXX -shared -fsanitize=thread -shared-libsan -o $O/libstellar_host.so $O/*.o -L. -lstellar_sigverify \
     -Wl,-rpath,"$R/stellar-core_amd" -Wl,-rpath,/opt/rocm/lib -lpthread
 python3 - "$R" > $O/stress.py <<'PY'
 import re, sys
 src = open(sys.argv[1] + "/tests/test_host_mirror.py").read()
 print(re.search(r'_POOL_STRESS = r"""(.*?)"""', src, re.S).group(1).replace("range(8000)", "range(300)"))
 PY
-TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$(gcc -print-file-name=libtsan.so) \
+TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$TSAN_RT \
     python3 $O/stress.py $O/libstellar_host.so "$R/tests/native/libhostcore.so" > $O/out.txt 2>&1 || true
 echo "pool stress: TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out.txt || true); result: $(tail -1 $O/out.txt)"
 # the micro-batcher (VerifyMicroBatcher: producer shards, flush workers,
@@ -43,7 +50,7 @@ for ff in (0, 1):
     assert ff or out.all()
 print("ok")
 PY
-TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$(gcc -print-file-name=libtsan.so) \
+TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$TSAN_RT \
     python3 $O/mb.py $O/libstellar_host.so "$R/tests/native/libhostcore.so" > $O/out_mb.txt 2>&1 || true
 echo "micro-batcher flood: TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out_mb.txt || true); result: $(tail -1 $O/out_mb.txt)"
 # the tx-set pre-pass (round 3): parallel marshal, SignatureBatchPrefetch::addBatch parts and
@@ -83,7 +90,7 @@ for _ in range(3):
     assert rc == 0, rc
 print("ok")
 PY
-TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$(gcc -print-file-name=libtsan.so) \
+TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$TSAN_RT \
     python3 $O/txset.py $O/libstellar_host.so "$R/tests/native/libhostcore.so" "$R" > $O/out_txset.txt 2>&1 || true
 echo "tx-set pre-pass + keyed walk: TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out_txset.txt || true); result: $(tail -1 $O/out_txset.txt)"
 # the C-ABI's slot-table lifetime (sv_shutdown / sv_set_device_map against

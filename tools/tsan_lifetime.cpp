@@ -8,6 +8,7 @@
 // an in-flight call is a TSan report (or a crash).  Built and run by
 // tools/tsan_host.sh; prints "ok <calls> <remaps>".
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -75,7 +76,9 @@ int main() {
         (void)sv_set_device_map(map, 1 + r % 3);
       }
       remaps.fetch_add(1);
-      std::this_thread::yield();
+      // (callers run between teardowns: the lock prefers the writer, so a
+      // back-to-back remap loop would otherwise leave them no turn)
+      std::this_thread::sleep_for(std::chrono::microseconds(500));
     }
     stop.store(true);
   });
@@ -83,6 +86,10 @@ int main() {
   sv_shutdown();
   if (bad.load()) {
     fprintf(stderr, "unexpected return codes: %ld\n", bad.load());
+    return 1;
+  }
+  if (calls.load() < 4 * remaps.load()) {
+    fprintf(stderr, "callers starved: %ld calls over %ld remaps\n", calls.load(), remaps.load());
     return 1;
   }
   printf("ok %ld %ld\n", calls.load(), remaps.load());
