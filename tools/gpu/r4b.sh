@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-r4b}; mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1 || exit $?
 V="base prevsha alias64 alias64k alias64both"
 LIBS=""; for v in $V; do LIBS="$LIBS variants/libsv_$v.so"; done
 AB_NOCHECK=alias AB_ROUNDS=${AB_ROUNDS:-8} timeout -k 10 400 python -u tools/ab_variants.py $LIBS > $OUT/ab.txt 2>&1 || exit $?
