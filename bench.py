@@ -513,9 +513,18 @@ def main():
         achieved = kernel_rate * W_MAD_PER_VERIFY / 1e12
         traffic = None
         prof = {}
-        tf = os.path.join(REPO, "profiles", "r03_traffic.json")
-        if not os.path.exists(tf):
-            tf = os.path.join(REPO, "profiles", "r02_traffic.json")
+        tf = None
+        for rnd in ("r04", "r03", "r02"):  # the newest profile measured on this kernel source wins
+            cand = os.path.join(REPO, "profiles", rnd + "_traffic.json")
+            if os.path.exists(cand):
+                try:
+                    with open(cand) as f:
+                        if json.load(f).get("kernel_source_sha256") == sv.kernel_source_digest():
+                            tf = cand
+                            break
+                except Exception:
+                    pass
+        tf = tf or os.path.join(REPO, "profiles", "r03_traffic.json")
         if os.path.exists(tf):
             try:
                 with open(tf) as f:
@@ -531,15 +540,17 @@ def main():
         # hardware multiply-adds the SIMDs issue per verify (tools/madcount.py,
         # SV_MADCOUNT build), when measured on this kernel source
         hw_mads, hw_src = None, None
-        mf = os.path.join(REPO, "profiles", "r03", "madcount.json")
+        mf = os.path.join(REPO, "profiles", "r04", "madcount.json")
+        if not os.path.exists(mf):
+            mf = os.path.join(REPO, "profiles", "r03", "madcount.json")
         if os.path.exists(mf):
             try:
                 with open(mf) as f:
                     mj = json.load(f)
                 if mj.get("kernel_source_sha256") == sv.kernel_source_digest():
                     hw_mads = float(mj["hw_mads_per_verify"])
-                    hw_src = ("profiles/r03/madcount.json (tools/madcount.py: prep %.0f + main %.0f per verify)"
-                              % (mj["prep_mads_per_verify"], mj["main_mads_per_verify"]))
+                    hw_src = ("%s (tools/madcount.py: prep %.0f + main %.0f per verify)"
+                              % (os.path.relpath(mf, REPO), mj["prep_mads_per_verify"], mj["main_mads_per_verify"]))
             except Exception:
                 hw_mads = None
         result = {

@@ -288,23 +288,21 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
 __device__ __forceinline__ int32_t sv_nibble(uint32_t word, int p) {
   return (int32_t)__builtin_amdgcn_sbfe((int)word, (unsigned)(4 * (p & 7)), 4u);
 }
-#ifndef SV_PF
-#define SV_PF 0
-#endif
-// L2 prefetch of a table entry's cache lines by LDS-DMA of one dword per lane
-// per 128-B line into a per-wave scratch word (no VGPR, nothing reads it): an
-// entry staged only one addition ahead of its use (R, B0, B1) then lands from
-// L2 instead of beyond it.  Lines touched by an entry of `bytes` at e: those
-// holding e, e + 128 and e + bytes - 4 (bytes <= 256).
-__device__ __forceinline__ void sv_l2_prefetch(const sv_u4* entry, int bytes, uint32_t* pf) {
-  const char* e = (const char*)entry;
-  __builtin_amdgcn_global_load_lds((const void*)e, (__attribute__((address_space(3))) void*)pf, 4, 0, 0);
-  __builtin_amdgcn_global_load_lds((const void*)(e + 128), (__attribute__((address_space(3))) void*)pf, 4, 0, 0);
-  __builtin_amdgcn_global_load_lds((const void*)(e + bytes - 4), (__attribute__((address_space(3))) void*)pf, 4, 0, 0);
+// The identity entry of every -A / -R table (digit 0), one copy per device:
+// the prep kernel does not write each signature's entry 0 (verify_core.h
+// sv_build_ltab) and the main kernel stages digit-0 additions from here (an
+// L2-resident line).
+__device__ sv_u4 sv_ident_lentry[SV_LTAB_QUADS] = {{1u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 1u, 0u},
+                                                    {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {1u, 0u, 0u, 0u},
+                                                    {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u},
+                                                    {0u, 0u, 0u, 0u}};
+__device__ __forceinline__ const sv_u4* sv_lentry_at(const sv_u4* tab, int32_t d) {
+  if (d == 0) return sv_ident_lentry;
+  return tab + (d < 0 ? -d : d) * SV_LTAB_QUADS;
 }
 __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw, uint32_t flags, int W,
                                                    const sv_u4* tabA, const sv_u4* tabR, const sv_u4* btab0,
-                                                   const sv_u4* btab1, sv_u4* stage, uint32_t* pf) {
+                                                   const sv_u4* btab1, sv_u4* stage) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const bool top8A = (flags & SV_REC_TOP8A) != 0, top8R = (flags & SV_REC_TOP8R) != 0;
   const bool rneg = (flags & SV_REC_RNEG) != 0;
@@ -321,11 +319,11 @@ __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw,
     if (rneg) dR = -dR;
     fe qa, qb, qz, qt;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    sv_stage_lentry(stage, tabA + (dA < 0 ? -dA : dA) * SV_LTAB_QUADS);
+    sv_stage_lentry(stage, sv_lentry_at(tabA, dA));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sv_load_lentry(qa, qb, qz, qt, stage + __lane_id(), 64, dA < 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    sv_stage_lentry(stage, tabR + (dR < 0 ? -dR : dR) * SV_LTAB_QUADS);
+    sv_stage_lentry(stage, sv_lentry_at(tabR, dR));
     fe_sub(P.X, qa, qb);
     fe_add(P.Y, qa, qb);
     fe_add(P.Z, qz, qz);
@@ -365,16 +363,15 @@ __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw,
     if (bwin) {
       dB0 = (int32_t)rw[16 + w / SV_LB_WIN];
       dB1 = (int32_t)rw[16 + SV_LB_DIGITS + w / SV_LB_WIN];
+#ifdef SV_DIAG_BTAB_ALIAS  // (diagnostic builds only: wrong verdicts; base-point entries from a small range)
+      dB0 %= SV_DIAG_BTAB_ALIAS;
+      dB1 %= SV_DIAG_BTAB_ALIAS;
+#endif
     }
     const int nsteps = bwin ? 8 : 6;
     const int s0 = (w == W - 1) ? 4 : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    sv_stage_lentry(stage, tabA + (dA < 0 ? -dA : dA) * SV_LTAB_QUADS);
-    if (SV_PF & 1) sv_l2_prefetch(tabR + (dR < 0 ? -dR : dR) * SV_LTAB_QUADS, 16 * SV_LTAB_QUADS, pf);
-    if ((SV_PF & 2) && bwin) {
-      sv_l2_prefetch(btab0 + (dB0 < 0 ? -dB0 : dB0) * SV_BTAB_QUADS, 4 * SV_BTAB_STRIDE, pf);
-      sv_l2_prefetch(btab1 + (dB1 < 0 ? -dB1 : dB1) * SV_BTAB_QUADS, 4 * SV_BTAB_STRIDE, pf);
-    }
+    sv_stage_lentry(stage, sv_lentry_at(tabA, dA));
     SV_NOUNROLL for (int s = s0; s < nsteps; ++s) {
       if (s < 4) {
         ge_dbl(Q, P.X, P.Y, P.Z);
@@ -390,7 +387,7 @@ __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw,
           sv_load_lentry(qa, qb, qz, qt, stage + __lane_id(), 64, neg);
           if (s == 4 || bwin) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (s == 4) sv_stage_lentry(stage, tabR + (dR < 0 ? -dR : dR) * SV_LTAB_QUADS);
+            if (s == 4) sv_stage_lentry(stage, sv_lentry_at(tabR, dR));
             else sv_stage_bentry(stage, btab0, dB0);
           }
         } else {
@@ -417,7 +414,6 @@ template <bool KT>
 __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cparams c) {
   const sv_kparams& p = c.k;
   __shared__ sv_u4 s_stage[SV_BLOCK / 64][SV_LTAB_QUADS * 64];  // per-wave entry stage
-  __shared__ uint32_t s_pf[SV_BLOCK / 64][64];                    // per-wave prefetch sink (SV_PF)
   const uint32_t lane = threadIdx.x & 63u;
   sv_u4* stage = s_stage[threadIdx.x >> 6];
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -443,7 +439,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cpa
     const bool pre_ok = (flags & SV_REC_OK) != 0;
     const int W = (int)__builtin_amdgcn_readfirstlane(c.wmax[li >> 6]);
     ge_p3 P;
-    sv_main_scalarmult(P, rw, flags, W, tabA, tabR, btab0, btab1, stage, s_pf[threadIdx.x >> 6]);
+    sv_main_scalarmult(P, rw, flags, W, tabA, tabR, btab0, btab1, stage);
     const bool ok = pre_ok && sv_is_identity(P) && active;
     if (active) p.verdict[c.start + li] = ok ? 1 : 0;
     const uint64_t mask = __ballot(ok);

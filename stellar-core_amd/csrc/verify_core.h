@@ -466,12 +466,18 @@ SV_HD void sv_load_lentry(fe& qa, fe& qb, fe& qz, fe& qt, const sv_u4* p, int qs
 
 // {0..8}·P in cached form into tab (9 entries x 10 quads, lane-contiguous).
 // P comes straight from ge_frombytes, so it is affine (Z = 1): each step adds
-// it with the mixed law (2 Z1 Z2 = 2 Z1, no product).
+// it with the mixed law (2 Z1 Z2 = 2 Z1, no product).  Device builds do not
+// write entry 0 (the identity): the main kernel stages digit 0 from one shared
+// copy (sv_kernels.hip sv_ident_lentry), 1 in 9 table bytes fewer written and,
+// for digit-0 windows, an L2-resident line read (A/B: -1.5 % / -4.9 % per 2^20
+// on two boxes, profiles/r04/ab_mem/).  Host builds (the CPU path) keep it.
 SV_COLD void sv_build_ltab(sv_u4* tab, const ge_p3& P) {
   ge_cached c1, ce;
   ge_p3_to_cached(c1, P);
   ge_cached_identity(ce);
+#if !defined(__HIP_DEVICE_COMPILE__)
   sv_store_lentry(tab, ce);
+#endif
   sv_store_lentry(tab + SV_LTAB_QUADS, c1);
   ge_p3 P3 = P;
   ge_p1p1 Q;

@@ -4,7 +4,7 @@
   python tools/save_profile.py gpurun_out/r1b/prof profiles/r01/<name>
 
 Copies the kernel-stats and counter CSVs plus summary.json, and rewrites
-profiles/r02_traffic.json (the file bench.py reads roofline.traffic from,
+profiles/<round>_traffic.json (the file bench.py reads roofline.traffic from,
 keyed by the verify kernel's source digest) from the summary.
 """
 import glob
@@ -40,7 +40,11 @@ def main():
         "kernel": s["kernel"],
         "kernel_source_sha256": s["kernel_source_sha256"],
     }
-    with open(os.path.join(repo, "profiles", "r02_traffic.json"), "w") as f:
+    # profiles/<round>_traffic.json, the round taken from the destination
+    # (profiles/r04/... -> r04); bench.py takes the newest one whose kernel
+    # digest matches the sources it runs
+    rnd = os.path.relpath(os.path.abspath(dst), os.path.join(repo, "profiles")).split(os.sep)[0]
+    with open(os.path.join(repo, "profiles", "%s_traffic.json" % rnd), "w") as f:
         json.dump(t, f, indent=1)
     print(json.dumps(t, indent=1))
 
