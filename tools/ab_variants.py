@@ -65,10 +65,11 @@ for rnd in range(ROUNDS):
         out = torch.zeros(n, dtype=torch.uint8, device=dev)
         t = timed(lib, out)
         o = out.cpu().numpy()
-        if want is None:
+        diag = any(t in name for t in os.environ.get("AB_NOCHECK", "").split(",") if t)
+        if want is None and not diag:
             want = o
             assert o.sum() == n - n // 8, o.sum()
-        if not any(t in name for t in os.environ.get("AB_NOCHECK", "").split(",") if t):
+        if not diag and want is not None:
             assert (o == want).all(), name + " verdict mismatch"
         has_split = hasattr(lib, "sv_set_debug_flags") and lib.sv_set_debug_flags(SV_DBG_PREP_ONLY) >= 0
         tp = float("nan")
