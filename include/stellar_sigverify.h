@@ -260,6 +260,15 @@ typedef struct sv_key_cache_stats {
 } sv_key_cache_stats;
 int sv_key_cache_get_stats(int device, sv_key_cache_stats* out);
 
+/* Host-side stages of the calling thread's last latency-lane batch (a batch of
+ * at most one staging chunk on one slot), in microseconds: out[0] plan + pack,
+ * [1] the H2D call, [2] the kernel launch, [3] the D2H / event record calls,
+ * [4] key-table build queueing, [5] the wait for the device (H2D + kernel +
+ * verdicts), [6] the whole batch inside the engine, [7] 1 if it ran the
+ * warm-key comb kernel, 0 the octet kernel.  Zeros before the first batch.
+ * For tail-latency diagnosis (bench.py latency_1k.slow_iterations). */
+int sv_lat_last_trace(double out[8]);
+
 /* Per-key tables of the throughput path (replaces, for repeated signers, the
  * per-signature decode of A that libsodium's verify does,
  * /root/reference/src/crypto/SecretKey.cpp:461-463 per call; catchup replays

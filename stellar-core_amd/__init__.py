@@ -142,6 +142,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sv_set_key_tables.argtypes = [ctypes.c_int, sz]
     lib.sv_key_cache_wait.argtypes = [ctypes.c_int]
     lib.sv_key_cache_get_stats.argtypes = [ctypes.c_int, ctypes.POINTER(KeyCacheStats)]
+    lib.sv_lat_last_trace.argtypes = [ctypes.POINTER(ctypes.c_double)]
     _lib = lib
     return lib
 
@@ -417,3 +418,14 @@ def key_cache_stats(device: int = 0) -> dict:
     st = KeyCacheStats()
     _check(load_library().sv_key_cache_get_stats(device, ctypes.byref(st)))
     return {f: int(getattr(st, f)) for f, _ in KeyCacheStats._fields_}
+
+
+LAT_TRACE_FIELDS = ("plan_pack_us", "h2d_call_us", "launch_us", "d2h_rec_us", "build_us", "sync_us", "total_us", "warm")
+
+
+def lat_last_trace() -> dict:
+    """Host-side stages of this thread's last latency-lane batch
+    (sv_lat_last_trace, include/stellar_sigverify.h), in microseconds."""
+    buf = (ctypes.c_double * 8)()
+    _check(load_library().sv_lat_last_trace(buf))
+    return dict(zip(LAT_TRACE_FIELDS, list(buf)))
