@@ -300,12 +300,9 @@ __device__ __forceinline__ const sv_u4* sv_lentry_at(const sv_u4* tab, int32_t d
   if (d == 0) return sv_ident_lentry;
   return tab + (d < 0 ? -d : d) * SV_LTAB_QUADS;
 }
-#ifndef SV_PFR
-#define SV_PFR 0
-#endif
 __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw, uint32_t flags, int W,
                                                    const sv_u4* tabA, const sv_u4* tabR, const sv_u4* btab0,
-                                                   const sv_u4* btab1, sv_u4* stage, uint32_t* pf) {
+                                                   const sv_u4* btab1, sv_u4* stage) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const bool top8A = (flags & SV_REC_TOP8A) != 0, top8R = (flags & SV_REC_TOP8R) != 0;
   const bool rneg = (flags & SV_REC_RNEG) != 0;
@@ -375,18 +372,6 @@ __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw,
     const int s0 = (w == W - 1) ? 4 : 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     sv_stage_lentry(stage, sv_lentry_at(tabA, dA));
-#if SV_PFR
-    {
-      // L2 prefetch of the R entry (staged only one addition ahead): one
-      // dword LDS-DMA per 128-B line into a sink; younger than A's DMAs, so
-      // the A step waits for all but these three
-      const char* e = (const char*)sv_lentry_at(tabR, dR);
-      __attribute__((address_space(3))) void* sink = (__attribute__((address_space(3))) void*)pf;
-      __builtin_amdgcn_global_load_lds((const void*)e, sink, 4, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(e + 128), sink, 4, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(e + 156), sink, 4, 0, 0);
-    }
-#endif
     SV_NOUNROLL for (int s = s0; s < nsteps; ++s) {
       if (s < 4) {
         ge_dbl(Q, P.X, P.Y, P.Z);
@@ -396,8 +381,7 @@ __device__ __forceinline__ void sv_main_scalarmult(ge_p3& P, const uint32_t* rw,
         const bool zone = s >= 6;
         // the entry DMA'd for this step (and any digit load) has landed; once
         // the entry is read, the stage receives the next addition's entry
-        if (SV_PFR && s == 4) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (!zone) {
           neg = (s == 4 ? dA : dR) < 0;
           sv_load_lentry(qa, qb, qz, qt, stage + __lane_id(), 64, neg);
@@ -430,7 +414,6 @@ template <bool KT>
 __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cparams c) {
   const sv_kparams& p = c.k;
   __shared__ sv_u4 s_stage[SV_BLOCK / 64][SV_LTAB_QUADS * 64];  // per-wave entry stage
-  __shared__ uint32_t s_pf[SV_BLOCK / 64][SV_PFR ? 64 : 1];        // per-wave prefetch sink (SV_PFR)
   const uint32_t lane = threadIdx.x & 63u;
   sv_u4* stage = s_stage[threadIdx.x >> 6];
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -456,7 +439,7 @@ __global__ __launch_bounds__(SV_BLOCK, SV_MAIN_WAVES) void sv_main_kernel(sv_cpa
     const bool pre_ok = (flags & SV_REC_OK) != 0;
     const int W = (int)__builtin_amdgcn_readfirstlane(c.wmax[li >> 6]);
     ge_p3 P;
-    sv_main_scalarmult(P, rw, flags, W, tabA, tabR, btab0, btab1, stage, s_pf[threadIdx.x >> 6]);
+    sv_main_scalarmult(P, rw, flags, W, tabA, tabR, btab0, btab1, stage);
     const bool ok = pre_ok && sv_is_identity(P) && active;
     if (active) p.verdict[c.start + li] = ok ? 1 : 0;
     const uint64_t mask = __ballot(ok);
