@@ -31,7 +31,19 @@ SV_HD uint32_t sv_ld32(const uint8_t* p, int64_t avail) {
 }
 
 SV_HD uint32_t sv_rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
-SV_HD uint64_t sv_rotr64b(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate (n a compile-time constant, 0 < n < 64): on the device two
+// v_alignbit_b32 on the halves, or a swap for n = 32 (LLVM otherwise emits
+// two 64-bit shifts and two ORs)
+SV_HD uint64_t sv_rotr64b(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (n == 32) return sv_pack64(hi, lo);
+  if (n < 32) return sv_pack64(__builtin_amdgcn_alignbit(hi, lo, n), __builtin_amdgcn_alignbit(lo, hi, n));
+  return sv_pack64(__builtin_amdgcn_alignbit(lo, hi, n - 32), __builtin_amdgcn_alignbit(hi, lo, n - 32));
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
 SV_HD uint32_t sv_bswap32b(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }
@@ -98,7 +110,7 @@ SV_COLD void sv_cache_key(uint32_t out[8], const uint32_t* pk, const uint32_t* s
         lo = sv_ld32(msg + o, (int64_t)len - o);
         hi = sv_ld32(msg + o + 4, (int64_t)len - o - 4);
       }
-      m[i] = ((uint64_t)hi << 32) | lo;
+      m[i] = sv_pack64(lo, hi);
     }
     const bool last = b + 1 == nb;
     blake2b_compress(h, m, last ? total : (b + 1) * 128, last);

@@ -48,7 +48,7 @@ SV_HD uint64_t sv_rotr64(uint64_t x, int n) {
     rlo = __builtin_amdgcn_alignbit(lo, hi, n - 32);
     rhi = __builtin_amdgcn_alignbit(hi, lo, n - 32);
   }
-  return ((uint64_t)rhi << 32) | rlo;
+  return sv_pack64(rlo, rhi);
 #else
   return (x >> n) | (x << (64 - n));
 #endif
@@ -58,7 +58,7 @@ SV_HD uint32_t sv_bswap32(uint32_t x) {
 }
 // big-endian 64-bit word from 8 little-endian-packed bytes held as two u32
 SV_HD uint64_t sv_be64(uint32_t lo_bytes, uint32_t hi_bytes) {
-  return ((uint64_t)sv_bswap32(lo_bytes) << 32) | sv_bswap32(hi_bytes);
+  return sv_pack64(sv_bswap32(hi_bytes), sv_bswap32(lo_bytes));
 }
 
 SV_HD void sha512_init(uint64_t st[8]) {
@@ -141,7 +141,7 @@ SV_HD uint64_t sv_msg_word(const uint8_t* m, uint32_t mlen, uint32_t mi) {
   const uint32_t lo = sh ? (d0 >> sh) | (d1 << (32 - sh)) : d0;
   const uint32_t hi = sh ? (d1 >> sh) | (d2 << (32 - sh)) : d1;
 #endif
-  uint64_t v = ((uint64_t)hi << 32) | lo;  // byte j of the word at bits 8j
+  uint64_t v = sv_pack64(lo, hi);  // byte j of the word at bits 8j
   if (mlen < mi + 8) {
     const uint32_t valid = mlen > mi ? mlen - mi : 0u;  // < 8
     v &= (1ull << (8 * valid)) - 1;

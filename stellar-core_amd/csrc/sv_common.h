@@ -44,6 +44,22 @@
 #define SV_NOUNROLL _Pragma("GCC unroll 1")
 #endif
 
+// 64-bit word from its 32-bit halves.  On the device as a bit cast of a
+// two-dword vector: LLVM turns the usual (hi << 32) | lo into a disjoint add
+// and then splits every 64-bit add of the result into a zero-extended
+// v_lshl_add_u64 plus a v_add_u32 on the high half (and v_movs to build the
+// zero-extended pairs): 55 -> 47 instructions per SHA-512 round with the
+// message schedule, 32 -> 29 without.
+SV_HD uint64_t sv_pack64(uint32_t lo, uint32_t hi) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
+  const u2_t v = {lo, hi};
+  return __builtin_bit_cast(uint64_t, v);
+#else
+  return ((uint64_t)hi << 32) | lo;
+#endif
+}
+
 // Three-input bit functions as gfx950's v_bitop3_b32 (any function of three
 // inputs by its 8-entry truth table, one VALU op per 32-bit half): xor3 (0x96,
 // the Sigma / sigma functions) and maj (0xE8).  LLVM emits two v_xor_b32 for
@@ -53,7 +69,7 @@ SV_HD uint64_t sv_xor3_64(uint64_t a, uint64_t b, uint64_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96);
   const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x96);
-  return ((uint64_t)hi << 32) | lo;
+  return sv_pack64(lo, hi);
 #else
   return a ^ b ^ c;
 #endif
@@ -69,7 +85,7 @@ SV_HD uint64_t sv_maj64(uint64_t a, uint64_t b, uint64_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xE8);
   const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xE8);
-  return ((uint64_t)hi << 32) | lo;
+  return sv_pack64(lo, hi);
 #else
   return (a & b) ^ (c & (a ^ b));
 #endif
