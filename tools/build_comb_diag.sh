@@ -1,0 +1,65 @@
+#!/bin/bash
+# Developer tool: timing-only diagnostic builds of the warm-key comb kernel
+# (wrong verdicts by design), linked with the product's other objects into
+# variants/libsv_diag_*.so for tools/ab_lat_capi.py.  The product sources are
+# not modified: each variant compiles a patched copy of sv_comb.hip.
+#   nodecode  decode wave: R's y only, no square root
+#   nohash    chain waves: no SHA-512 (hram from R ^ A and S)
+#   both      both of the above
+#   phases    the product's arithmetic plus per-wave s_memrealtime stamps at
+#             the phase boundaries, read back by sv_diag_comb_times()
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p variants/build
+C=stellar-core_amd/csrc
+T=$(mktemp -d)
+cp $C/*.h $C/sv_comb.hip $T/
+python3 - "$T" <<'PY'
+import sys
+t = sys.argv[1]
+src = open(t + "/sv_comb.hip").read()
+dec_a = "      ok = ge_frombytes(Rp, R, false) && ok;"
+dec_b = "      fe_frombytes(Rp.Y, R);\n      Rp.X = Rp.Y;"
+hash_a = "  sv_load_and_hash<MODE>(p, gi, A, S, hram);"
+hash_b = ("  {\n    uint32_t R_[8];\n    sv_unpack2(A, p.pk + 2 * gi);\n    sv_unpack2(R_, p.sig + 4 * gi);\n"
+          "    sv_unpack2(S, p.sig + 4 * gi + 2);\n"
+          "    for (int i = 0; i < 8; ++i) { hram[i] = R_[i] ^ A[i]; hram[8 + i] = S[i]; }\n  }")
+assert dec_a in src and hash_a in src
+open(t + "/comb_nodecode.hip", "w").write(src.replace(dec_a, dec_b))
+open(t + "/comb_nohash.hip", "w").write(src.replace(hash_a, hash_b))
+open(t + "/comb_both.hip", "w").write(src.replace(dec_a, dec_b).replace(hash_a, hash_b))
+# phase stamps: wave w of workgroup b writes stamp k to sv_diag_t[b][w][k]
+ph = src
+hdr = ("__device__ unsigned long long sv_diag_t[1024][4][8];\n"
+       "#define SV_DT(k) do { SV_FENCE(); const unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); "
+       "SV_FENCE(); if (__lane_id() == 0 && blockIdx.x < 1024) sv_diag_t[blockIdx.x][wave][k] = t_; } while (0)\n")
+anchor = "// One signature per SPW-th of a chain wave; see the file header."
+assert anchor in ph
+ph = ph.replace(anchor, hdr + anchor)
+reps = [
+  ("  if (wave == 0) {\n", "  SV_DT(0);\n  if (wave == 0) {\n"),
+  ("      s_rok[lane] = ok ? 1u : 0u;\n    }\n    __syncthreads();\n", "      s_rok[lane] = ok ? 1u : 0u;\n    }\n    SV_DT(1);\n    __syncthreads();\n    SV_DT(2);\n"),
+  (hash_a, hash_a + "\n  SV_DT(1);"),
+  ("  sc_digits_r256(dB, S);\n", "  sc_digits_r256(dB, S);\n  SV_DT(2);\n"),
+  ("  qo_from_cached(P, ent[0], q, eneg[0]);\n", "  qo_from_cached(P, ent[0], q, eneg[0]);\n  SV_DT(3);\n"),
+  ("  SV_UNROLL for (int t = 1; t < NE; ++t) qo_add(P, ent[t], q, eneg[t]);\n", "  SV_UNROLL for (int t = 1; t < NE; ++t) qo_add(P, ent[t], q, eneg[t]);\n  SV_DT(4);\n"),
+  ("  __syncthreads();  // x_R, y_R from the decode wave\n", "  SV_DT(5);\n  __syncthreads();  // x_R, y_R from the decode wave\n  SV_DT(6);\n"),
+  ("  if (active && quad == 0 && role == 0) p.verdict[g] = ok ? 1 : 0;\n}", "  if (active && quad == 0 && role == 0) p.verdict[g] = ok ? 1 : 0;\n  SV_DT(7);\n}"),
+  ('extern "C" {\n', 'extern "C" {\n\nint sv_diag_comb_times(void* out, size_t bytes) {\n  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sv_diag_t), bytes);\n}\n'),
+]
+for a, b in reps:
+    assert ph.count(a) == 1, a
+    ph = ph.replace(a, b)
+open(t + "/comb_phases.hip", "w").write(ph)
+PY
+for v in nodecode nohash both phases; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -c $T/comb_$v.hip -o variants/build/comb_$v.o &
+done
+wait
+B=stellar-core_amd/build
+for v in nodecode nohash both phases; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/libsv_diag_$v.so $B/sv_kernels.o variants/build/comb_$v.o \
+      $B/sv_api.o $B/sv_hash.o $B/sv_cpu.o -Wl,-rpath,/opt/rocm/lib -lpthread
+done
+rm -rf $T
+ls -la variants/libsv_diag_*.so
