@@ -42,9 +42,10 @@ def pytest_configure(config):
 
 
 def _make(dirpath, target):
+    # make every time: the Makefiles list the headers, so an edited header
+    # rebuilds the library instead of testing a stale one
     path = os.path.join(dirpath, target)
-    if not os.path.exists(path):
-        subprocess.run(["make", "-s"], cwd=dirpath, check=True)
+    subprocess.run(["make", "-s", target], cwd=dirpath, check=True)
     return path
 
 
