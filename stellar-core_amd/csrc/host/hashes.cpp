@@ -2,6 +2,7 @@
 // Checked against Python hashlib in tests/test_host_mirror.py.
 #include "hashes.h"
 
+#include <cstdlib>
 #include <cstring>
 
 #if defined(__x86_64__)
@@ -65,11 +66,11 @@ __attribute__((target("avx2"))) void blake2b_compress_avx2(uint64_t h[8], const 
                                _mm256_setr_epi64x((long long)t0, (long long)t1, last ? -1LL : 0LL, 0LL));
   const __m256i a0 = a, b0 = b;
 #define SV_B2_G(mx, my)                                                            \
-  a = _mm256_add_epi64(_mm256_add_epi64(a, b), mx);                                \
+  a = _mm256_add_epi64(_mm256_add_epi64(a, mx), b);                                \
   d = _mm256_shuffle_epi32(_mm256_xor_si256(d, a), _MM_SHUFFLE(2, 3, 0, 1));       \
   c = _mm256_add_epi64(c, d);                                                      \
   b = _mm256_shuffle_epi8(_mm256_xor_si256(b, c), r24);                            \
-  a = _mm256_add_epi64(_mm256_add_epi64(a, b), my);                                \
+  a = _mm256_add_epi64(_mm256_add_epi64(a, my), b);                                \
   d = _mm256_shuffle_epi8(_mm256_xor_si256(d, a), r16);                            \
   c = _mm256_add_epi64(c, d);                                                      \
   b = _mm256_xor_si256(b, c);                                                      \
@@ -95,10 +96,62 @@ __attribute__((target("avx2"))) void blake2b_compress_avx2(uint64_t h[8], const 
   _mm256_storeu_si256((__m256i*)(h + 4), _mm256_xor_si256(b0, _mm256_xor_si256(b, d)));
 }
 const bool kHaveAvx2 = __builtin_cpu_supports("avx2");
+
+// AVX-512VL form (chosen at run time where the host has it): the same four
+// rows, every G's message vector ONE two-table permute (vpermt2q) of the 16
+// message words held in two 512-bit registers instead of four scalar inserts,
+// and the rotations single vprorq instructions.  (In both vector forms the
+// message word is added to a before b: b is the end of the previous G's
+// dependency chain, a + m is not.)
+__attribute__((target("avx512f,avx512vl"))) void blake2b_compress_avx512(uint64_t h[8], const uint8_t* block,
+                                                                         uint64_t t0, uint64_t t1, bool last) {
+  const __m512i mlo = _mm512_loadu_si512((const void*)block);
+  const __m512i mhi = _mm512_loadu_si512((const void*)(block + 64));
+  __m256i a = _mm256_loadu_si256((const __m256i*)h);
+  __m256i b = _mm256_loadu_si256((const __m256i*)(h + 4));
+  __m256i c = _mm256_loadu_si256((const __m256i*)kIV);
+  __m256i d = _mm256_xor_si256(_mm256_loadu_si256((const __m256i*)(kIV + 4)),
+                               _mm256_setr_epi64x((long long)t0, (long long)t1, last ? -1LL : 0LL, 0LL));
+  const __m256i a0 = a, b0 = b;
+#define SV_B5_G(mx, my)                                 \
+  a = _mm256_add_epi64(_mm256_add_epi64(a, mx), b);     \
+  d = _mm256_ror_epi64(_mm256_xor_si256(d, a), 32);     \
+  c = _mm256_add_epi64(c, d);                           \
+  b = _mm256_ror_epi64(_mm256_xor_si256(b, c), 24);     \
+  a = _mm256_add_epi64(_mm256_add_epi64(a, my), b);     \
+  d = _mm256_ror_epi64(_mm256_xor_si256(d, a), 16);     \
+  c = _mm256_add_epi64(c, d);                           \
+  b = _mm256_ror_epi64(_mm256_xor_si256(b, c), 63);
+#define SV_B5_M(r, i, j, k, l)                                                                                  \
+  _mm512_castsi512_si256(_mm512_permutex2var_epi64(                                                           \
+      mlo, _mm512_setr_epi64(kSigma[r][i], kSigma[r][j], kSigma[r][k], kSigma[r][l], 0, 0, 0, 0), mhi))
+#define SV_B5_ROUND(r)                                                        \
+  SV_B5_G(SV_B5_M(r, 0, 2, 4, 6), SV_B5_M(r, 1, 3, 5, 7))                     \
+  b = _mm256_permute4x64_epi64(b, _MM_SHUFFLE(0, 3, 2, 1));                   \
+  c = _mm256_permute4x64_epi64(c, _MM_SHUFFLE(1, 0, 3, 2));                   \
+  d = _mm256_permute4x64_epi64(d, _MM_SHUFFLE(2, 1, 0, 3));                   \
+  SV_B5_G(SV_B5_M(r, 8, 10, 12, 14), SV_B5_M(r, 9, 11, 13, 15))               \
+  b = _mm256_permute4x64_epi64(b, _MM_SHUFFLE(2, 1, 0, 3));                   \
+  c = _mm256_permute4x64_epi64(c, _MM_SHUFFLE(1, 0, 3, 2));                   \
+  d = _mm256_permute4x64_epi64(d, _MM_SHUFFLE(0, 3, 2, 1));
+  SV_B5_ROUND(0) SV_B5_ROUND(1) SV_B5_ROUND(2) SV_B5_ROUND(3) SV_B5_ROUND(4) SV_B5_ROUND(5)
+  SV_B5_ROUND(6) SV_B5_ROUND(7) SV_B5_ROUND(8) SV_B5_ROUND(9) SV_B5_ROUND(10) SV_B5_ROUND(11)
+#undef SV_B5_ROUND
+#undef SV_B5_M
+#undef SV_B5_G
+  _mm256_storeu_si256((__m256i*)h, _mm256_xor_si256(a0, _mm256_xor_si256(a, c)));
+  _mm256_storeu_si256((__m256i*)(h + 4), _mm256_xor_si256(b0, _mm256_xor_si256(b, d)));
+}
+const bool kHaveAvx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") &&
+                         getenv("SVH_NO_AVX512") == nullptr;
 #endif
 
 void Blake2b256::compress(bool last) {
 #if defined(__x86_64__)
+  if (kHaveAvx512) {
+    blake2b_compress_avx512(h_, buf_, t_[0], t_[1], last);
+    return;
+  }
   if (kHaveAvx2) {
     blake2b_compress_avx2(h_, buf_, t_[0], t_[1], last);
     return;

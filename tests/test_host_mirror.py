@@ -121,6 +121,24 @@ def test_blake2b256_and_sha256_match_hashlib(host):
         assert out.raw == hashlib.sha256(b).digest(), n
 
 
+def test_blake2b256_without_avx512_matches_hashlib():
+    """The AVX2 / scalar compression (hosts without AVX-512VL) in a process
+    that opts out of the AVX-512 path (SVH_NO_AVX512)."""
+    import subprocess
+    import sys
+    code = (
+        "import ctypes, hashlib, os\n"
+        "lib = ctypes.CDLL(%r)\n"
+        "out = ctypes.create_string_buffer(32)\n"
+        "for n in (0, 1, 127, 128, 129, 256, 352, 1000):\n"
+        "    b = bytes((i * 131 + n) & 255 for i in range(n))\n"
+        "    lib.svh_blake2b256(out, b, ctypes.c_size_t(n))\n"
+        "    assert out.raw == hashlib.blake2b(b, digest_size=32).digest(), n\n"
+        % os.path.join(REPO, "stellar-core_amd", "libstellar_host.so"))
+    env = dict(os.environ, SVH_NO_AVX512="1")
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=120)
+
+
 def test_verify_sig_cache_semantics(host, engine, golden):
     d = golden["valid"]
     pk, sig = d["pk"][0].tobytes(), d["sig"][0].tobytes()
