@@ -501,9 +501,14 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
 // wave 0 adds the result at the end (second LDS handoff).
 #define SV_OCTET_BLOCK 128
 
+// The tables (23 KB) are dynamic LDS, placed after the static arrays below:
+// measured 2.2 us faster per cold 1k batch than the same tables as the first
+// static array (0.2428 -> 0.2406 ms, 8 of 8 rounds, profiles/r04/ab_octlds/).
+#define SV_OCTET_TAB_BYTES (SV_OSIGS * 2 * SV_ATAB_ENTRIES * SV_QENT_DW * 4)
 template <int MODE>
 __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams p) {
-  __shared__ uint32_t s_tab[SV_OSIGS][2][SV_ATAB_ENTRIES][SV_QENT_DW];  // 23 KB
+  extern __shared__ uint32_t s_dyn[];
+  uint32_t(*s_tab)[2][SV_ATAB_ENTRIES][SV_QENT_DW] = (uint32_t(*)[2][SV_ATAB_ENTRIES][SV_QENT_DW])s_dyn;
   __builtin_amdgcn_s_setprio(3);  // latency class (as sv_comb_kernel)
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t role = lane & 3u, half = (lane >> 2) & 1u, sl = lane >> 3;
@@ -924,11 +929,11 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
   if (path == 2) {  // SV_PATH_LATENCY
     const unsigned og = (unsigned)((n + SV_OSIGS - 1) / SV_OSIGS);
     if (mode == 0)
-      hipLaunchKernelGGL(sv_octet_kernel<0>, dim3(og), dim3(SV_OCTET_BLOCK), 0, s, p);
+      hipLaunchKernelGGL(sv_octet_kernel<0>, dim3(og), dim3(SV_OCTET_BLOCK), SV_OCTET_TAB_BYTES, s, p);
     else if (mode == 1)
-      hipLaunchKernelGGL(sv_octet_kernel<1>, dim3(og), dim3(SV_OCTET_BLOCK), 0, s, p);
+      hipLaunchKernelGGL(sv_octet_kernel<1>, dim3(og), dim3(SV_OCTET_BLOCK), SV_OCTET_TAB_BYTES, s, p);
     else
-      hipLaunchKernelGGL(sv_octet_kernel<2>, dim3(og), dim3(SV_OCTET_BLOCK), 0, s, p);
+      hipLaunchKernelGGL(sv_octet_kernel<2>, dim3(og), dim3(SV_OCTET_BLOCK), SV_OCTET_TAB_BYTES, s, p);
     return hipGetLastError();
   }
   (void)path;
