@@ -460,6 +460,10 @@ int64_t share_window_ns() {
   static const int64_t w = (int64_t)env_size("SV_LAT_SHARE_MS", 1000) * 1000000;
   return w;
 }
+size_t share_upload_bytes() {
+  static const size_t b = std::max<size_t>(64, env_size("SV_SHARE_UPLOAD_KB", 2048)) * 1024;
+  return b;
+}
 bool share_now(const Device& D) {
   const int64_t w = share_window_ns();
   return w > 0 && now_ns() - D.lat_last_ns.load(std::memory_order_relaxed) < w;
@@ -919,7 +923,14 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     trace_at("staging");
     if (P == 1) {
       pack(in, lo, m, im, hp);
-      SV_HIP(hipMemcpyAsync(s.d_in.p, s.h_in.p, im.bytes, hipMemcpyHostToDevice, up_s));
+      // While latency-lane batches are live (shared mode), a chunk goes up in
+      // pieces of SV_SHARE_UPLOAD_KB (default 2048): a 1k batch's 370 KB copy
+      // otherwise queues behind the whole 32 MB chunk copy (~0.65 ms, once per
+      // chunk: profiles/r04/isolation/).
+      const size_t piece = share_now(D) ? share_upload_bytes() : im.bytes;
+      for (size_t o = 0; o < im.bytes; o += piece)
+        SV_HIP(hipMemcpyAsync((uint8_t*)s.d_in.p + o, (const uint8_t*)s.h_in.p + o, std::min(piece, im.bytes - o),
+                              hipMemcpyHostToDevice, up_s));
       if (!single) {
         SV_HIP(hipEventRecord(s.up, D.h2d));
         SV_HIP(hipStreamWaitEvent(D.stream, s.up, 0));
