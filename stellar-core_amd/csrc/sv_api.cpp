@@ -744,6 +744,11 @@ bool stage_trace() {
   return t;
 }
 thread_local double g_trace_pack_us = 0;
+// (both traces also print steady-clock microseconds, to line a bulk call's
+// stages up with the latency lane's batches)
+double trace_abs_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // Collects a finished chunk's results from its pinned slot.
 int drain_stage(Stage& s, uint8_t* verdict, uint8_t* keys) {
@@ -870,8 +875,9 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
   int tables = -1;
   auto trace_at = [](const char* what) {
     if (stage_trace())
-      fprintf(stderr, "SV_STAGE_TRACE %s at %.1f us\n", what,
-              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - g_trace_t0).count());
+      fprintf(stderr, "SV_STAGE_TRACE %s at %.1f us @%.1f\n", what,
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - g_trace_t0).count(),
+              trace_abs_us());
   };
   // the largest launch first, so the workspace never grows under a running kernel
   if (verdict && (rc = ensure_ws(D, sv_verify_ws_bytes(resolve_path(path, chunk), grid_for(D, chunk), chunk))))
@@ -898,6 +904,7 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     // slot c & 1 was last used by chunk c - 2: its results are collected
     // (which also means its H2D, kernels and D2H are complete)
     if ((rc = drain_stage(s, verdict, keys))) return rc;
+    trace_at("slot drained");
     m = single ? n : chunk_len(c, chunk, n - lo);
     size_t msg_total;
     const Image im = image_of(in, lo, m, &msg_total);
@@ -931,6 +938,7 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
       for (size_t o = 0; o < im.bytes; o += piece)
         SV_HIP(hipMemcpyAsync((uint8_t*)s.d_in.p + o, (const uint8_t*)s.h_in.p + o, std::min(piece, im.bytes - o),
                               hipMemcpyHostToDevice, up_s));
+      trace_at("uploads enqueued");
       if (!single) {
         SV_HIP(hipEventRecord(s.up, D.h2d));
         SV_HIP(hipStreamWaitEvent(D.stream, s.up, 0));
@@ -995,6 +1003,7 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
       if ((rc = launch_locked(D, mode, path, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m,
                               s.d_verdict.p, nullptr, tables != 0)))
         return rc;
+      trace_at("launched");
     }
     if (!single) {
       SV_HIP(hipEventRecord(s.done, D.stream));
@@ -1110,6 +1119,7 @@ int lat_ready(Device& D) {
   SV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   SV_HIP(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, greatest));
   L.z_out.mapped = true;
+  L.h_in.mapped = true;  // (the kernels read it in place: lat_in_place)
   L.ready = true;  // (release_lat cleans up whatever exists from here on)
   hipError_t e = hipStreamCreateWithPriority(&L.build, hipStreamNonBlocking, least);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.ev_lat, hipEventDisableTiming);
@@ -1285,8 +1295,7 @@ void lat_build(LatLane& L) {
 // Zero-copy verdicts (SV_LAT_ZERO_COPY, default on): the kernel of a
 // verdict-only latency batch writes its verdicts straight into mapped pinned
 // memory, which saves the blit dispatch of a D2H copy (~6 us of a ~0.12 ms
-// batch, tools/gpu/api_probe.hip).  The input image still goes up by one H2D
-// copy: kernels reading it in place over the fabric ran ~11 us longer.
+// batch, tools/gpu/api_probe.hip).
 
 std::atomic<int> g_lat_zc{-1};
 bool lat_zero_copy() {
@@ -1297,6 +1306,18 @@ bool lat_zero_copy() {
     g_lat_zc.store(v);
   }
   return v != 0;
+}
+
+// Input read in place (SV_LAT_ZC_IN, default on; 0: one staged H2D copy):
+// the kernels read the packed image straight from mapped pinned memory.  The
+// kernel runs longer (+10 us at 1k signatures, reads over the fabric) but the
+// H2D dispatch is gone: p50 1000 / 4096 / 12288 warm 0.116 / 0.261 / 0.551 ->
+// 0.112 / 0.253 / 0.508 ms, and a staged copy queues behind a bulk call's
+// chunk upload (up to ~0.8 ms per 32 MB chunk): p99 under the 2^22 host
+// batch 0.61-0.86 -> 0.22 ms (profiles/r04/isolation/).
+bool lat_in_place() {
+  static const bool b = env_size("SV_LAT_ZC_IN", 1) != 0;
+  return b;
 }
 
 std::atomic<int> g_lat_trace{-1};
@@ -1313,7 +1334,7 @@ bool lat_trace() {
 thread_local std::array<double, 8> t_lat_last{};
 
 // One latency-bound host batch on the slot's latency lane: pinned image (+
-// the key slots when warm), one H2D, [hash kernel, keys D2H], the comb kernel
+// the key slots when warm) read in place (or one H2D), [hash kernel, keys D2H], the comb kernel
 // (every key cached) or the octet kernel, one D2H, one sync.
 int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, const KeysCb& kcb,
                      bool* cb_done) {
@@ -1333,7 +1354,8 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   const size_t in_bytes = warm ? o_ks + 4 * n : im.bytes;
   const size_t out_per = (verdict ? 1 : 0) + (keys ? 32 : 0);
   const bool zc = verdict && !keys && lat_zero_copy();
-  if ((rc = L.h_in.ensure(in_bytes)) || (rc = L.d_in.ensure(in_bytes))) return rc;
+  const bool in_place = lat_in_place();
+  if ((rc = L.h_in.ensure(in_bytes)) || (!in_place && (rc = L.d_in.ensure(in_bytes)))) return rc;
   if (zc) {
     if ((rc = L.z_out.ensure(n))) return rc;
   } else {
@@ -1345,9 +1367,9 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   pack(in, 0, n, im, h);
   if (warm) std::memcpy(h + o_ks, L.kslots.data(), 4 * n);
   const auto t1 = std::chrono::steady_clock::now();
-  SV_HIP(hipMemcpyAsync(L.d_in.p, h, in_bytes, hipMemcpyHostToDevice, L.stream));
+  if (!in_place) SV_HIP(hipMemcpyAsync(L.d_in.p, h, in_bytes, hipMemcpyHostToDevice, L.stream));
   const auto t_up = std::chrono::steady_clock::now();
-  uint8_t* d = (uint8_t*)L.d_in.p;
+  uint8_t* d = (uint8_t*)(in_place ? L.h_in.dp : L.d_in.p);
   void* d_verdict = zc ? L.z_out.dp : L.d_out.p;
   const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
   const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
@@ -1406,9 +1428,9 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   if (lat_trace()) {
     fprintf(stderr,
             "SV_LAT_TRACE n=%zu %s plan+pack %.1f us | h2d call %.1f launch %.1f d2h+rec %.1f build %.1f sync %.1f"
-            " | device %.1f us\n",
+            " | device %.1f us @%.1f%s\n",
             n, warm ? "warm" : "cold", us(t0, t1), us(t1, t_up), us(t_up, t_k), us(t_k, t_down), us(t_down, t_b),
-            us(t_b, t2), us(t1, t2));
+            us(t_b, t2), us(t1, t2), trace_abs_us() - us(t0, t2), in_place ? " in place" : "");
   }
   return SV_OK;
 }

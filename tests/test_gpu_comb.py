@@ -10,8 +10,15 @@ keys for a table build.  Both must give libsodium's verdict on every row:
   * an SCP-shaped set (100 validator keys, 0..400-byte messages, mutated rows)
     at sizes that select each kernel geometry (1, 2 and 4 signatures per
     chain wave), against the oracle;
-  * eviction: a cache smaller than the key set still gives exact verdicts.
+  * eviction: a cache smaller than the key set still gives exact verdicts;
+  * the staged-copy lane (SV_LAT_ZC_IN=0 / SV_LAT_ZERO_COPY=0: one H2D of the
+    image, one D2H of the verdicts) gives the same verdicts as the default
+    (kernels read the image and write the verdicts in mapped memory).
 """
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -126,3 +133,47 @@ def test_cache_off_is_octet_only(sv, gpu, golden):
         assert sv.key_cache_stats(0)["warm_batches"] == w0
     finally:
         sv.set_key_cache(1024)
+
+
+_STAGED_CHILD = r"""
+import ctypes, os, sys
+import numpy as np
+import torch  # noqa: F401  (the HIP runtime torch ships, as in the parent)
+z = np.load(sys.argv[2], allow_pickle=False)
+lib = ctypes.CDLL(os.path.join(sys.argv[1], "stellar-core_amd", "libstellar_sigverify.so"))
+class Opts(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32), ("max_devices", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+opts = Opts(ctypes.sizeof(Opts), 0, 0, 0x2)  # SV_FLAG_PATH_LATENCY
+arrs = [np.ascontiguousarray(z[k]) for k in ("pk", "sig", "msg", "msg_off", "msg_len")]
+n = len(arrs[4])
+assert lib.sv_init() == 0
+outs = []
+for it in range(12):  # cold first, warm once the keys are built
+    out = np.zeros(n, np.uint8)
+    rc = lib.sv_ed25519_verify_batch(*[ctypes.c_void_p(a.ctypes.data) for a in arrs], ctypes.c_size_t(n),
+                                     ctypes.c_void_p(out.ctypes.data), ctypes.byref(opts))
+    assert rc == 0, rc
+    outs.append(out)
+    if it == 1:
+        assert lib.sv_key_cache_wait(0) == 0
+np.save(sys.argv[3], np.stack(outs))
+"""
+
+
+def test_staged_copy_lane_matches(sv, gpu, oracle, tmp_path):
+    """The lane with its staged copies (env switches read once per process,
+    hence a child process) against the oracle, cold and warm."""
+    d = _scp_set(oracle, 1000, seed=77)
+    src = tmp_path / "set.npz"
+    np.savez(src, pk=d["pk"], sig=d["sig"], msg=d["msg"], msg_off=d["msg_off"].astype(np.uint64),
+             msg_len=d["msg_len"].astype(np.uint32))
+    dst = tmp_path / "out.npy"
+    env = dict(os.environ, SV_LAT_ZC_IN="0", SV_LAT_ZERO_COPY="0")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _STAGED_CHILD, repo, str(src), str(dst)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    outs = np.load(dst, allow_pickle=False)
+    for it, out in enumerate(outs):
+        assert (out == d["verdict"]).all(), (it, np.nonzero(out != d["verdict"])[0][:10])

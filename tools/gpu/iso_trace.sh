@@ -5,4 +5,5 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-iso_trace}; mkdir -p $OUT
 export TMPDIR=/tmp
+if [ -n "$STAGE" ]; then export SV_STAGE_TRACE=1; fi  # (the bulk calls' stages too)
 SV_LAT_TRACE=1 SV_ISOLATION_OUT=$OUT/isolation_shared.json timeout -k 10 300 python -u -m pytest tests/test_gpu_isolation.py -x -q -s --timeout 240 --timeout-method thread > $OUT/iso.txt 2> $OUT/trace.txt || exit $?
