@@ -134,6 +134,7 @@ __global__ __launch_bounds__(256, 1) void sv_comb_kernel(sv_comb_params c) {
   const sv_kparams& p = c.k;
   __shared__ uint32_t s_r[NS][20];  // x_R, y_R (10 limbs each)
   __shared__ uint32_t s_rok[NS];
+  __shared__ sv_u4 s_msg[NS][SV_MSG_CAP / 16];  // messages (sv_load_and_hash_lds)
   const uint32_t lane = __lane_id();
   const uint64_t gbase = (uint64_t)blockIdx.x * NS;
   // wave-uniform, visibly so (a scalar branch around the barrier)
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(256, 1) void sv_comb_kernel(sv_comb_params c) {
   const uint64_t gi = active ? g : p.n - 1;  // idle tail signatures redo the last item
 
   uint32_t A[8], S[8], hram[16];
-  sv_load_and_hash<MODE>(p, gi, A, S, hram);
+  sv_load_and_hash_lds<MODE, LPS>(p, gi, lane % LPS, s_msg[ls], A, S, hram);
   const uint32_t ks = c.kslot[gi];
   const uint32_t kst = c.kstat[ks];
   uint32_t h[8], dA[8], dB[8];

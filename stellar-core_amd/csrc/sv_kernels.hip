@@ -505,7 +505,12 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
 // measured 2.2 us faster per cold 1k batch than the same tables as the first
 // static array (0.2428 -> 0.2406 ms, 8 of 8 rounds, profiles/r04/ab_octlds/).
 #define SV_OCTET_TAB_BYTES (SV_OSIGS * 2 * SV_ATAB_ENTRIES * SV_QENT_DW * 4)
-template <int MODE>
+// + the hash wave's message windows (sv_load_and_hash_lds), after the tables.
+// MSG: launches of at most one workgroup per CU (n <= 8 per CU) only; larger
+// ones read the message from memory (the extra 4 KB would cost a
+// workgroup slot per CU: 12288 cold 0.58 -> 0.80 ms).
+#define SV_OCTET_LDS_BYTES(MSG) (SV_OCTET_TAB_BYTES + ((MSG) ? SV_OSIGS * SV_MSG_CAP : 0))
+template <int MODE, bool MSG>
 __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams p) {
   extern __shared__ uint32_t s_dyn[];
   uint32_t(*s_tab)[2][SV_ATAB_ENTRIES][SV_QENT_DW] = (uint32_t(*)[2][SV_ATAB_ENTRIES][SV_QENT_DW])s_dyn;
@@ -531,7 +536,12 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     sv_unpack2(A, p.pk + 2 * ii);
     sv_unpack2(R, p.sig + 4 * ii);
   } else {
-    sv_load_and_hash<MODE>(p, ii, A, S, hram);
+    if (MSG) {
+      sv_u4* s_msg = (sv_u4*)(s_dyn + SV_OCTET_TAB_BYTES / 4);
+      sv_load_and_hash_lds<MODE, 8>(p, ii, lane & 7u, s_msg + sl * (SV_MSG_CAP / 16), A, S, hram);
+    } else {
+      sv_load_and_hash<MODE>(p, ii, A, S, hram);
+    }
     sv_unpack2(R, p.sig + 4 * ii);
   }
   bool ok = true;
@@ -928,12 +938,15 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
   p.dbg = dbg;
   if (path == 2) {  // SV_PATH_LATENCY
     const unsigned og = (unsigned)((n + SV_OSIGS - 1) / SV_OSIGS);
-    if (mode == 0)
-      hipLaunchKernelGGL(sv_octet_kernel<0>, dim3(og), dim3(SV_OCTET_BLOCK), SV_OCTET_TAB_BYTES, s, p);
-    else if (mode == 1)
-      hipLaunchKernelGGL(sv_octet_kernel<1>, dim3(og), dim3(SV_OCTET_BLOCK), SV_OCTET_TAB_BYTES, s, p);
-    else
-      hipLaunchKernelGGL(sv_octet_kernel<2>, dim3(og), dim3(SV_OCTET_BLOCK), SV_OCTET_TAB_BYTES, s, p);
+    const bool msg = og <= sv_device_simds() / 4;
+#define SV_OCTET_LAUNCH(M, G) \
+  hipLaunchKernelGGL((sv_octet_kernel<M, G>), dim3(og), dim3(SV_OCTET_BLOCK), SV_OCTET_LDS_BYTES(G), s, p)
+    if (mode == 0) SV_OCTET_LAUNCH(0, false);  // (32-byte messages: no window)
+    else if (mode == 1 && msg) SV_OCTET_LAUNCH(1, true);
+    else if (mode == 1) SV_OCTET_LAUNCH(1, false);
+    else if (msg) SV_OCTET_LAUNCH(2, true);
+    else SV_OCTET_LAUNCH(2, false);
+#undef SV_OCTET_LAUNCH
     return hipGetLastError();
   }
   (void)path;

@@ -44,3 +44,41 @@ __device__ __forceinline__ void sv_load_and_hash(const sv_kparams& p, uint64_t i
     sha512_ram_var(hram, R, A, p.msg + ii * (uint64_t)p.fixed_len, p.fixed_len);
   }
 }
+
+// The latency kernels' loader (sv_comb_kernel chain waves, sv_octet_kernel
+// hash wave).  Their input image lives in mapped host memory (the lane reads
+// it in place), where every dependent round trip costs ~2 us: a message read
+// word by word inside the SHA-512 blocks pays one per block.  Here the LPS
+// lanes of a signature first copy the 16-byte-aligned window holding its
+// message into LDS (lbuf, SV_MSG_CAP bytes; one 16-byte load per lane per
+// LPS * 16 bytes), so the message costs one round trip after the offset's,
+// and the hash reads LDS.  A longer message is hashed from memory as before.
+#define SV_MSG_CAP 512
+template <int MODE, int LPS>
+__device__ __forceinline__ void sv_load_and_hash_lds(const sv_kparams& p, uint64_t ii, uint32_t li, sv_u4* lbuf,
+                                                     uint32_t A[8], uint32_t S[8], uint32_t hram[16]) {
+  if (MODE == 0) {  // (32-byte messages come with R, A and S in one round trip)
+    sv_load_and_hash<0>(p, ii, A, S, hram);
+    return;
+  }
+  uint32_t R[8];
+  sv_unpack2(A, p.pk + 2 * ii);
+  sv_unpack2(R, p.sig + 4 * ii);
+  sv_unpack2(S, p.sig + 4 * ii + 2);
+  const uint8_t* mp = MODE == 1 ? p.msg + p.msg_off[ii] : p.msg + ii * (uint64_t)p.fixed_len;
+  const uint32_t mlen = MODE == 1 ? p.msg_len[ii] : p.fixed_len;
+  // (an aligned 16-byte block never crosses a page: reading the whole first
+  // and last block of the message stays inside mapped memory)
+  const uint32_t lead = (uint32_t)((uintptr_t)mp & 15u);
+  const uint32_t nq = (lead + mlen + 15u) >> 4;
+  const bool fits = nq <= SV_MSG_CAP / 16;
+  if (fits) {
+    const sv_u4* src = (const sv_u4*)(mp - lead);
+    for (uint32_t c = li; c < nq; c += LPS) lbuf[c] = src[c];
+  }
+  // (the lanes of one wave: LDS is in order within the wave)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  sha512_ram_var(hram, R, A, fits ? (const uint8_t*)lbuf + lead : mp, mlen);
+}

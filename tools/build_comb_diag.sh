@@ -22,7 +22,7 @@ t = sys.argv[1]
 src = open(t + "/sv_comb.hip").read()
 dec_a = "      ok = ge_frombytes(Rp, R, false) && ok;"
 dec_b = "      fe_frombytes(Rp.Y, R);\n      Rp.X = Rp.Y;"
-hash_a = "  sv_load_and_hash<MODE>(p, gi, A, S, hram);"
+hash_a = "  sv_load_and_hash_lds<MODE, LPS>(p, gi, lane % LPS, s_msg[ls], A, S, hram);"
 hash_b = ("  {\n    uint32_t R_[8];\n    sv_unpack2(A, p.pk + 2 * gi);\n    sv_unpack2(R_, p.sig + 4 * gi);\n"
           "    sv_unpack2(S, p.sig + 4 * gi + 2);\n"
           "    for (int i = 0; i < 8; ++i) { hram[i] = R_[i] ^ A[i]; hram[8 + i] = S[i]; }\n  }")
@@ -58,7 +58,7 @@ ok = open(t + "/sv_kernels.hip").read()
 ohdr = ("__device__ unsigned long long sv_diag_o[2048][2][8];\n"
         "#define SV_OT(k) do { SV_FENCE(); const unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); "
         "SV_FENCE(); if (__lane_id() == 0 && blockIdx.x < 2048) sv_diag_o[blockIdx.x][threadIdx.x >> 6][k] = t_; } while (0)\n")
-anchor = "template <int MODE>\n__global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel"
+anchor = "template <int MODE, bool MSG>\n__global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel"
 assert ok.count(anchor) == 1
 ok = ok.replace(anchor, ohdr + anchor)
 oreps = [
@@ -77,9 +77,9 @@ for a, b in oreps:
     assert ok.count(a) == 1, a
     ok = ok.replace(a, b)
 # hash wave: stamp 1 after the hash (the decode wave's stamp 1 is its square roots)
-a = "  } else {\n    sv_load_and_hash<MODE>(p, ii, A, S, hram);\n    sv_unpack2(R, p.sig + 4 * ii);\n  }\n  bool ok = true;"
+a = "    sv_unpack2(R, p.sig + 4 * ii);\n  }\n  bool ok = true;"
 assert ok.count(a) == 1
-ok = ok.replace(a, "  } else {\n    sv_load_and_hash<MODE>(p, ii, A, S, hram);\n    sv_unpack2(R, p.sig + 4 * ii);\n    SV_OT(1);\n  }\n  bool ok = true;")
+ok = ok.replace(a, "    sv_unpack2(R, p.sig + 4 * ii);\n    SV_OT(1);\n  }\n  bool ok = true;")
 open(t + "/kernels_ophases.hip", "w").write(ok)
 PY
 for v in nodecode nohash both phases; do
