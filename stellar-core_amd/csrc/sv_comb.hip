@@ -129,12 +129,11 @@ __global__ __launch_bounds__(256, 1) void sv_comb_kernel(sv_comb_params c) {
   constexpr int QPS = LPS / 4;                   // quads per signature
   constexpr int PA = SV_KA_POS / QPS;            // -A positions per quad
   constexpr int PB = SV_CB_POS / QPS;            // B positions per quad
-  constexpr int NE = PA + PB;                    // entries per quad
   static_assert(PB >= 2 && PA % 4 == 0, "geometry");
   const sv_kparams& p = c.k;
   __shared__ uint32_t s_r[NS][20];  // x_R, y_R (10 limbs each)
   __shared__ uint32_t s_rok[NS];
-  __shared__ sv_u4 s_msg[NS][SV_MSG_CAP / 16];  // messages (sv_load_and_hash_lds)
+  __shared__ sv_u4 s_msg[SV_COMB_CHAIN_WAVES][SPW * (SV_MSG_CAP / 16)];  // message windows
   const uint32_t lane = __lane_id();
   const uint64_t gbase = (uint64_t)blockIdx.x * NS;
   // wave-uniform, visibly so (a scalar branch around the barrier)
@@ -167,29 +166,51 @@ __global__ __launch_bounds__(256, 1) void sv_comb_kernel(sv_comb_params c) {
   const bool active = g < p.n;
   const uint64_t gi = active ? g : p.n - 1;  // idle tail signatures redo the last item
 
+  // Hash first (the message through its LDS window, sv_load_and_hash_lds),
+  // then the quad's entries in two groups, B then -A: fewer entries live at
+  // once than loading all of them together (SPW = 4: 256 -> 229 VGPRs, 4096
+  // warm 0.216 -> 0.199 ms in A/B, profiles/r04/lane_msg_lds/).
   uint32_t A[8], S[8], hram[16];
-  sv_load_and_hash_lds<MODE, LPS>(p, gi, lane % LPS, s_msg[ls], A, S, hram);
+  sv_load_and_hash_lds<MODE, LPS>(p, gi, lane % LPS, s_msg[wave - 1] + sw * (SV_MSG_CAP / 16), A, S, hram);
   const uint32_t ks = c.kslot[gi];
   const uint32_t kst = c.kstat[ks];
-  uint32_t h[8], dA[8], dB[8];
-  sc_reduce512(h, hram);
   const bool s_ok = sc_is_canonical(S);
   // a lane with S >= L is rejected by (1); clearing bits 253..255 keeps its
   // radix-256 digits inside the table (top digit <= 32); every S < 2^253,
   // so every S < L, is left unchanged
   S[7] &= 0x1fffffffu;
-  sc_digits_r16(dA, h);
+  uint32_t dB[8];
   sc_digits_r256(dB, S);
-
-  // this quad's entries: -A positions quad*PA + t, B positions quad*PB + t
-  const uint32_t* ka = c.ktab + (size_t)ks * SV_KEY_SLOT_DW;
-  fe ent[NE];
-  bool eneg[NE];
+  // this quad's entries: B positions quad*PB + t, -A positions quad*PA + t
+  fe entB[PB];
+  bool negB[PB];
   {
-    constexpr int WA = PA >= 8 ? PA / 8 : 1, WB = PB >= 4 ? PB / 4 : 1;
-    uint32_t wa[WA], wb[WB];
-    SV_UNROLL for (int u = 0; u < WA; ++u) wa[u] = sv_pick8(dA, ((quad * PA) >> 3) + u);
+    constexpr int WB = PB >= 4 ? PB / 4 : 1;
+    uint32_t wb[WB];
     SV_UNROLL for (int u = 0; u < WB; ++u) wb[u] = sv_pick8(dB, ((quad * PB) >> 2) + u);
+    SV_UNROLL for (int t = 0; t < PB; ++t) {
+      const uint32_t k = PB >= 4 ? (uint32_t)(t & 3) : ((quad * PB) & 3) + t;
+      const int32_t e = sv_sbyte(wb[PB >= 4 ? t >> 2 : 0], k);
+      negB[t] = e < 0;
+      const uint32_t pos = quad * PB + t;
+      ce_load(entB[t], c.ctab + (pos * SV_CB_ENT + (uint32_t)(e < 0 ? -e : e)) * SV_CE_DW, role, e < 0);
+    }
+  }
+  // the quad's partial sum, B half
+  fe P;
+  qo_from_cached(P, entB[0], q, negB[0]);
+  SV_UNROLL for (int t = 1; t < PB; ++t) qo_add(P, entB[t], q, negB[t]);
+  uint32_t h[8], dA[8];
+  sc_reduce512(h, hram);
+  sc_digits_r16(dA, h);
+  // -A half
+  const uint32_t* ka = c.ktab + (size_t)ks * SV_KEY_SLOT_DW;
+  {
+    constexpr int WA = PA >= 8 ? PA / 8 : 1;
+    uint32_t wa[WA];
+    SV_UNROLL for (int u = 0; u < WA; ++u) wa[u] = sv_pick8(dA, ((quad * PA) >> 3) + u);
+    fe ent[PA];
+    bool eneg[PA];
     SV_UNROLL for (int t = 0; t < PA; ++t) {
       const uint32_t k = PA >= 8 ? (uint32_t)(t & 7) : ((quad * PA) & 7) + t;
       const int32_t d = sv_snib(wa[PA >= 8 ? t >> 3 : 0], k);
@@ -197,18 +218,8 @@ __global__ __launch_bounds__(256, 1) void sv_comb_kernel(sv_comb_params c) {
       const uint32_t pos = quad * PA + t;
       ce_load(ent[t], ka + (pos * SV_KA_ENT + (uint32_t)(d < 0 ? -d : d)) * SV_CE_DW, role, d < 0);
     }
-    SV_UNROLL for (int t = 0; t < PB; ++t) {
-      const uint32_t k = PB >= 4 ? (uint32_t)(t & 3) : ((quad * PB) & 3) + t;
-      const int32_t e = sv_sbyte(wb[PB >= 4 ? t >> 2 : 0], k);
-      eneg[PA + t] = e < 0;
-      const uint32_t pos = quad * PB + t;
-      ce_load(ent[PA + t], c.ctab + (pos * SV_CB_ENT + (uint32_t)(e < 0 ? -e : e)) * SV_CE_DW, role, e < 0);
-    }
+    SV_UNROLL for (int t = 0; t < PA; ++t) qo_add(P, ent[t], q, eneg[t]);
   }
-  // the quad's partial sum
-  fe P;
-  qo_from_cached(P, ent[0], q, eneg[0]);
-  SV_UNROLL for (int t = 1; t < NE; ++t) qo_add(P, ent[t], q, eneg[t]);
   // tree over the signature's quads: quad k (k % 2s == 0) adds quad k + s
   SV_UNROLL for (int s = 1; s < QPS; s *= 2) {
     fe cp, mine;
