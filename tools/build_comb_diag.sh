@@ -22,7 +22,7 @@ t = sys.argv[1]
 src = open(t + "/sv_comb.hip").read()
 dec_a = "      ok = ge_frombytes(Rp, R, false) && ok;"
 dec_b = "      fe_frombytes(Rp.Y, R);\n      Rp.X = Rp.Y;"
-hash_a = "  sv_load_and_hash_lds<MODE, LPS>(p, gi, lane % LPS, s_msg[ls], A, S, hram);"
+hash_a = "  sv_load_and_hash_lds<MODE, LPS>(p, gi, lane % LPS, s_msg[wave - 1] + sw * (SV_MSG_CAP / 16), A, S, hram);"
 hash_b = ("  {\n    uint32_t R_[8];\n    sv_unpack2(A, p.pk + 2 * gi);\n    sv_unpack2(R_, p.sig + 4 * gi);\n"
           "    sv_unpack2(S, p.sig + 4 * gi + 2);\n"
           "    for (int i = 0; i < 8; ++i) { hram[i] = R_[i] ^ A[i]; hram[8 + i] = S[i]; }\n  }")
@@ -43,8 +43,8 @@ reps = [
   ("      s_rok[lane] = ok ? 1u : 0u;\n    }\n    __syncthreads();\n", "      s_rok[lane] = ok ? 1u : 0u;\n    }\n    SV_DT(1);\n    __syncthreads();\n    SV_DT(2);\n"),
   (hash_a, hash_a + "\n  SV_DT(1);"),
   ("  sc_digits_r256(dB, S);\n", "  sc_digits_r256(dB, S);\n  SV_DT(2);\n"),
-  ("  qo_from_cached(P, ent[0], q, eneg[0]);\n", "  qo_from_cached(P, ent[0], q, eneg[0]);\n  SV_DT(3);\n"),
-  ("  SV_UNROLL for (int t = 1; t < NE; ++t) qo_add(P, ent[t], q, eneg[t]);\n", "  SV_UNROLL for (int t = 1; t < NE; ++t) qo_add(P, ent[t], q, eneg[t]);\n  SV_DT(4);\n"),
+  ("  qo_from_cached(P, entB[0], q, negB[0]);\n", "  qo_from_cached(P, entB[0], q, negB[0]);\n  SV_DT(3);\n"),
+  ("    SV_UNROLL for (int t = 0; t < PA; ++t) qo_add(P, ent[t], q, eneg[t]);\n  }\n", "    SV_UNROLL for (int t = 0; t < PA; ++t) qo_add(P, ent[t], q, eneg[t]);\n  }\n  SV_DT(4);\n"),
   ("  __syncthreads();  // x_R, y_R from the decode wave\n", "  SV_DT(5);\n  __syncthreads();  // x_R, y_R from the decode wave\n  SV_DT(6);\n"),
   ("  if (active && quad == 0 && role == 0) p.verdict[g] = ok ? 1 : 0;\n}", "  if (active && quad == 0 && role == 0) p.verdict[g] = ok ? 1 : 0;\n  SV_DT(7);\n}"),
   ('extern "C" {\n', 'extern "C" {\n\nint sv_diag_comb_times(void* out, size_t bytes) {\n  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(sv_diag_t), bytes);\n}\n'),

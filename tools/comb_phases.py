@@ -86,8 +86,8 @@ def main():
     span = (st[:, 1:, 7].max() - t0) * TICK_US
     print("workgroups %d, kernel span (first stamp -> last stamp) %.1f us" % (nwg, span))
     chain = st[:, 1:, :]
-    names = ["hash (load + SHA-512)", "mod L + digits", "entry loads + first entry", "sum (NE-1 additions)",
-             "tree", "barrier wait (decode wave)", "final check"]
+    names = ["hash (load + SHA-512)", "key slot + S digits", "B entry loads + first entry",
+             "B sum, mod L, -A loads + sum", "tree", "barrier wait (decode wave)", "final check"]
     print("chain waves (per wave, us): median / p90 / max")
     for k, nm in enumerate(names):
         d = (chain[:, :, k + 1] - chain[:, :, k]).ravel() * TICK_US
