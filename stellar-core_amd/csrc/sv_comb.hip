@@ -19,15 +19,17 @@
 //
 // Kernel geometry (sv_comb_kernel): 4 waves per workgroup, one per SIMD.
 //   wave 0  decodes R of the workgroup's signatures (one lane each: the
-//           square-root exponentiation, the longest serial chain) and hands
-//           (x_R, y_R, ok) over in LDS;
+//           square-root exponentiation, 57 us at 1k) and hands (x_R, y_R,
+//           ok) over in LDS;
 //   waves 1-3 ("chain waves") each verify SPW signatures: every lane hashes
-//           its signature (SHA-512, mod L, signed digits), then the 16/SPW
-//           lane quads of a signature each load their share of the 96 entries
-//           and add them with every point addition split over the quad's four
-//           lanes (own form, quad.h), and the quads' partial sums meet in a
-//           tree (DPP / ds_bpermute).  After one barrier the root quad tests
-//           Q == R_pt.
+//           its signature (SHA-512 over the message's LDS window, mod L,
+//           signed digits), then the 16/SPW lane quads of a signature each
+//           load their share of the 96 entries (B, then -A) and add them with
+//           every point addition split over the quad's four lanes (own form,
+//           quad.h), and the quads' partial sums meet in a tree (DPP /
+//           ds_bpermute).  After one barrier the root quad tests Q == R_pt.
+//           (62 us at 1k: the longer half, since the lane's image is read
+//           from host memory; profiles/r04/lane_msg_lds/.)
 // A 1000-signature batch with SPW = 2 is 167 workgroups: at most one per CU,
 // every wave alone on its SIMD.
 #include <hip/hip_runtime.h>
