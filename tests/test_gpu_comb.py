@@ -105,6 +105,45 @@ def test_fixed32_messages_warm(sv, cache, golden):
     assert (out == want).all()
 
 
+@pytest.mark.parametrize("mlen", [1, 100, 497, 600])
+def test_fixed_other_length_messages_warm(sv, cache, oracle, mlen):
+    """Fixed-length messages other than 32 bytes (MODE 2) on the comb kernel:
+    windows starting at several alignments (100: multiples of 4 mod 16; 497:
+    every alignment, filling up to all 32 quads of the 512-byte window), 1
+    and 600 (no window: hashed from memory)."""
+    import ctypes
+    rng = np.random.default_rng(mlen)
+    keys = []
+    for _ in range(20):
+        pkb, skb = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+        oracle.oracle_ed25519_seed_keypair(pkb, skb, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+        keys.append((pkb.raw, skb.raw))
+    n = 240
+    pk = np.zeros((n, 32), np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    msg = rng.integers(0, 256, (n, mlen), dtype=np.uint8)
+    for i in range(n):
+        pkb, skb = keys[i % 20]
+        sb = ctypes.create_string_buffer(64)
+        oracle.oracle_ed25519_sign(sb, msg[i].tobytes(), mlen, skb)
+        pk[i] = np.frombuffer(pkb, np.uint8)
+        sig[i] = np.frombuffer(sb.raw, np.uint8)
+    want = np.ones(n, np.uint8)
+    sig[::7, 33] ^= 0x10  # S bit
+    want[::7] = 0
+    msg[3::11, mlen - 1] ^= 0x01  # last message byte
+    want[3::11] = 0
+    for _ in range(8):
+        w0 = sv.key_cache_stats(0)["warm_batches"]
+        out = sv.verify_fixed(pk, sig, msg, mlen, device=0, path="latency")
+        assert (out == want).all(), np.nonzero(out != want)[0][:10]
+        if sv.key_cache_stats(0)["warm_batches"] == w0 + 1:
+            break
+        sv.key_cache_wait(0)
+    else:
+        raise AssertionError("never warm")
+
+
 def test_small_cache_evicts_exactly(sv, gpu, oracle):
     """A 64-key cache under a 100-key workload keeps evicting; verdicts stay
     exact whichever kernel serves each batch."""
