@@ -262,7 +262,7 @@ int sv_key_cache_get_stats(int device, sv_key_cache_stats* out);
 
 /* Host-side stages of the calling thread's last latency-lane batch (a batch of
  * at most one staging chunk on one slot), in microseconds: out[0] plan + pack,
- * [1] the H2D call, [2] the kernel launch, [3] the D2H / event record calls,
+ * [1] the H2D call (0 while the kernels read the image in place), [2] the kernel launch, [3] the D2H / event record calls,
  * [4] key-table build queueing, [5] the wait for the device (H2D + kernel +
  * verdicts), [6] the whole batch inside the engine, [7] 1 if it ran the
  * warm-key comb kernel, 0 the octet kernel.  Zeros before the first batch.

@@ -121,7 +121,9 @@ def run_isolation(sv, torch, oracle, host_n=1 << 22, dev_n=1 << 24, seed=3, idle
             t = time.perf_counter()
             out = lat_batch()
             dt = time.perf_counter() - t
-            lats.append((t, dt * 1e3))
+            # (the engine's own time for the batch, sv_lat_last_trace: the
+            # wall time above also holds this thread's Python and GIL waits)
+            lats.append((t, dt * 1e3, sv.lat_last_trace()["total_us"] / 1e3))
             if not np.array_equal(out, want):
                 errors.append(int(np.count_nonzero(out != want)))
 
@@ -137,9 +139,10 @@ def run_isolation(sv, torch, oracle, host_n=1 << 22, dev_n=1 << 24, seed=3, idle
     st1 = sv.key_cache_stats(0)
     res["bulk_loaded_ms"] = {k: (b - a) * 1e3 for k, (a, b) in phases.items()}
     for k, (a, b) in phases.items():
-        res["latency_during_" + k] = _summary([dt for t, dt in lats if a <= t < b])
-    res["latency_during_bulk"] = _summary([dt for t, dt in lats
-                                           if any(a <= t < b for a, b in phases.values())])
+        res["latency_during_" + k] = _summary([dt for t, dt, _ in lats if a <= t < b])
+    in_bulk = [(dt, de) for t, dt, de in lats if any(a <= t < b for a, b in phases.values())]
+    res["latency_during_bulk"] = _summary([dt for dt, _ in in_bulk])
+    res["engine_latency_during_bulk"] = _summary([de for _, de in in_bulk])
     res["warm_batches"] = st1["warm_batches"] - st0["warm_batches"]
     res["cold_batches"] = st1["cold_batches"] - st0["cold_batches"]
     res["shared_launches"] = st1["shared_launches"] - st0["shared_launches"]
