@@ -246,6 +246,7 @@ struct Device {
   hipEvent_t dep_in = nullptr, dep_out = nullptr;
   std::mutex mu;
   Stage st[2];
+  HostBuf z_in;  // mapped: a one-chunk batch's image, read in place (bulk_in_place)
   DevBuf msg, off, len, keys;  // sha256 batches
   HostBuf h_sha;
   // timing
@@ -320,6 +321,7 @@ int init_device(Device& D) {
   SV_HIP(hipStreamCreateWithFlags(&D.d2h, hipStreamNonBlocking));
   SV_HIP(hipEventCreateWithFlags(&D.dep_in, hipEventDisableTiming));
   SV_HIP(hipEventCreateWithFlags(&D.dep_out, hipEventDisableTiming));
+  D.z_in.mapped = true;
   for (Stage& s : D.st) {
     SV_HIP(hipEventCreateWithFlags(&s.up, hipEventDisableTiming));
     SV_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
@@ -346,6 +348,7 @@ void release_device(Device& D) {
   }
   D.pending.clear();
   D.pending_n.clear();
+  D.z_in.release();
   for (Stage& s : D.st) {
     s.h_in.release(); s.h_out.release();
     s.d_in.release(); s.d_verdict.release(); s.d_keys.release();
@@ -462,6 +465,15 @@ int64_t share_window_ns() {
 }
 size_t share_upload_bytes() {
   static const size_t b = std::max<size_t>(64, env_size("SV_SHARE_UPLOAD_KB", 2048)) * 1024;
+  return b;
+}
+// One-chunk host batches (n <= SV_STAGE_CHUNK) read in place
+// (SV_BULK_ZC_IN, default on; 0: one staged H2D copy): the kernels read the
+// packed image from mapped pinned memory, so the copy no longer runs before
+// the first kernel (a multi-chunk batch overlaps its copies with the previous
+// chunk's kernels and stays staged).
+bool bulk_in_place() {
+  static const bool b = env_size("SV_BULK_ZC_IN", 1) != 0;
   return b;
 }
 bool share_now(const Device& D) {
@@ -908,19 +920,22 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     m = single ? n : chunk_len(c, chunk, n - lo);
     size_t msg_total;
     const Image im = image_of(in, lo, m, &msg_total);
-    if ((rc = s.h_in.ensure(im.bytes)) || (rc = s.d_in.ensure(im.bytes)) || (rc = s.h_out.ensure(out_per * m)))
-      return rc;
-    if (verdict && (rc = s.d_verdict.ensure(m))) return rc;
-    if (keys && (rc = s.d_keys.ensure(32 * m))) return rc;
-    uint8_t* d = (uint8_t*)s.d_in.p;
-    uint8_t* hp = (uint8_t*)s.h_in.p;
-    const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
-    const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
     const bool early = single && kcb && keys && verdict;
     // a one-chunk keyed batch with a keys-ready callback: pack, copy up, hash
     // and copy the keys down in pieces, so the caller's walk starts early
     const std::vector<size_t> pb = early ? key_pieces(m) : std::vector<size_t>{0, m};
     const size_t P = pb.size() - 1;
+    const bool in_place = single && P == 1 && bulk_in_place();
+    HostBuf& hin = in_place ? D.z_in : s.h_in;
+    if ((rc = hin.ensure(im.bytes)) || (!in_place && (rc = s.d_in.ensure(im.bytes))) ||
+        (rc = s.h_out.ensure(out_per * m)))
+      return rc;
+    if (verdict && (rc = s.d_verdict.ensure(m))) return rc;
+    if (keys && (rc = s.d_keys.ensure(32 * m))) return rc;
+    uint8_t* d = (uint8_t*)(in_place ? D.z_in.dp : s.d_in.p);
+    uint8_t* hp = (uint8_t*)hin.p;
+    const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
+    const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
     while (s.pev.size() < P) {
       hipEvent_t e;
       SV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -935,7 +950,7 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
       // otherwise queues behind the whole 32 MB chunk copy (~0.65 ms, once per
       // chunk: profiles/r04/isolation/).
       const size_t piece = share_now(D) ? share_upload_bytes() : im.bytes;
-      for (size_t o = 0; o < im.bytes; o += piece)
+      for (size_t o = 0; !in_place && o < im.bytes; o += piece)
         SV_HIP(hipMemcpyAsync((uint8_t*)s.d_in.p + o, (const uint8_t*)s.h_in.p + o, std::min(piece, im.bytes - o),
                               hipMemcpyHostToDevice, up_s));
       trace_at("uploads enqueued");
@@ -2144,6 +2159,7 @@ int sv_pinned_bytes(int device, size_t* bytes) {
   std::lock_guard<std::mutex> g(Dp->mu);
   size_t b = 0;
   for (Stage& s : Dp->st) b += s.h_in.cap + s.h_out.cap;
+  b += Dp->z_in.cap;
   *bytes = b;
   return SV_OK;
 }

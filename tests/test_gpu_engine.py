@@ -115,7 +115,7 @@ def test_config5_64m_device_api(sv, dev, oracle):
 def test_host_api_pipeline_multi_chunk(sv, dev):
     """Host buffers larger than several staging chunks (2^18 signatures): the
     pipelined packing / H2D / kernels / D2H gives every row's verdict and pins
-    at most two chunks."""
+    at most two chunks (plus the in-place image of one-chunk batches)."""
     n = (1 << 18) * 3 + 12345
     tpk, tsig, tm = random_dataset(sv, dev, n, 7)
     pk, sig, msg = tpk.cpu().numpy(), tsig.cpu().numpy(), tm.cpu().numpy()
@@ -127,7 +127,7 @@ def test_host_api_pipeline_multi_chunk(sv, dev):
     want[bad] = 0
     assert np.array_equal(out, want)
     chunk_img = (1 << 18) * (128 + 1)
-    assert sv.pinned_bytes(0) <= 2 * 1.25 * chunk_img + (1 << 20)
+    assert sv.pinned_bytes(0) <= 3 * 1.25 * chunk_img + (1 << 20)
     # the same rows through the variable-length form, messages stored out of order
     perm = rng.permutation(n)
     buf = np.ascontiguousarray(msg[perm]).reshape(-1)  # buf row j = message perm[j]
