@@ -200,6 +200,37 @@ int svh_mb_run_workers(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg
                        const uint32_t* msg_len, size_t n, int producers, int workers, uint32_t max_batch,
                        uint32_t max_delay_us, uint32_t inter_arrival_us, uint8_t* verdict, svh_mb_stats* stats);
 
+/* Config 4 through the integration path (BASELINE config 4):
+ * `producers` overlay threads submit the n envelopes (pk, sig, msg) in bursts
+ * of `burst` (burst k starts interval_us * k after the run starts; interval_us
+ * 0 = a flood, back to back) into ONE VerifyMicroBatcher with the continuation
+ * form of submit(): each verdict's continuation posts the envelope to a "main
+ * thread", which calls PubKeyUtils::verifySig on it as HerderImpl::
+ * verifyEnvelope does (/root/reference/src/herder/HerderImpl.cpp:2414-2432)
+ * -- the reference's order: the overlay thread's pre-verify (Peer.cpp:963-970)
+ * completes before the message is posted to the main thread.
+ * verdict[i]: the main thread's verifySig result.  policy 0 WhenIdle, 1
+ * Deadline (VerifyMicroBatcher.h). */
+typedef struct svh_scp_params {
+  uint32_t struct_size; /* sizeof(svh_scp_params) */
+  uint32_t producers, burst, interval_us;
+  uint32_t max_batch, max_delay_us, workers;
+  uint32_t policy, linger_us, idle_in_flight;
+} svh_scp_params;
+typedef struct svh_scp_result {
+  double verdict_p50_us, verdict_p90_us, verdict_p99_us, verdict_max_us, verdict_mean_us; /* submit -> continuation */
+  double main_p50_us, main_p99_us;   /* submit -> the main thread's verifySig returned */
+  double main_call_p50_us;           /* one verifySig call on the main thread */
+  uint64_t main_hits, main_misses, main_mismatches; /* main-thread verifySig: cache hits / misses / != continuation */
+  uint64_t batches, flushed_by_size, flushed_by_deadline, flushed_idle, max_batch;
+  double mean_batch;
+  uint64_t gpu_batches, gpu_signatures, cpu_signatures, fallbacks; /* engine counts over the run */
+  double wall_s; /* first submission -> last main-thread verifySig */
+} svh_scp_result;
+int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                const uint32_t* msg_len, size_t n, const svh_scp_params* params, uint8_t* verdict,
+                svh_scp_result* result);
+
 #ifdef __cplusplus
 }
 #endif

@@ -393,6 +393,7 @@ RandomEvictionCache gVerifySigCache(0xffff);
 uint64_t gVerifyCacheHit = 0;
 uint64_t gVerifyCacheMiss = 0;
 uint64_t gBatchId = 0;  // owner ids of pending entries (under the mutex)
+thread_local uint64_t tVerifySigHits = 0, tVerifySigMisses = 0;  // flushThreadVerifySigCounts
 std::atomic<uint64_t> gGpuSigs{0}, gGpuBatches{0}, gCpuSigs{0}, gFallbacks{0};
 // batch-size and latency histograms (log2 buckets), per path
 std::atomic<uint64_t> gHist[4][PubKeyUtils::EngineHistograms::kBuckets];
@@ -935,9 +936,11 @@ bool verifySig(PublicKey const& key, Signature const& signature, ByteSlice const
     const uint32_t id = gVerifySigCache.find(k);
     if (id != RandomEvictionCache::kNone && gVerifySigCache.at(id).owner == 0) {
       ++gVerifyCacheHit;
+      ++tVerifySigHits;
       return gVerifySigCache.touch(id).value;
     }
   }
+  ++tVerifySigMisses;
   std::vector<VerifyItem> one{VerifyItem{&key, ByteSlice(signature), bin}};
   return verifySigBatch(one, nullptr)[0];
 }
@@ -958,6 +961,12 @@ void flushVerifySigCacheCounts(uint64_t& hits, uint64_t& misses) {
   misses = gVerifyCacheMiss;
   gVerifyCacheHit = 0;
   gVerifyCacheMiss = 0;
+}
+
+void flushThreadVerifySigCounts(uint64_t& hits, uint64_t& misses) {
+  hits = tVerifySigHits;
+  misses = tVerifySigMisses;
+  tVerifySigHits = tVerifySigMisses = 0;
 }
 
 void setBatchVerifierForTesting(BatchVerifyFn fn) { gTestVerifier.store(fn); }

@@ -143,6 +143,12 @@ void verifyBatchUncached(const uint8_t* pk, const uint8_t* sig, const uint8_t* m
 void clearVerifySigCache();
 void maybeSeedVerifySigCache(unsigned int seed);
 void flushVerifySigCacheCounts(uint64_t& hits, uint64_t& misses);
+// Hits / misses of the calling thread's own verifySig calls since its last
+// call of this function (flushes them).  Diagnostic: a caller that follows an
+// earlier pre-verify (HerderImpl::verifyEnvelope after Peer.cpp's) learns
+// whether its calls were served from the cache, which the process-wide
+// counters above cannot tell while other threads verify.
+void flushThreadVerifySigCounts(uint64_t& hits, uint64_t& misses);
 
 // BLAKE2b-256(pk || sig || msg), SecretKey.cpp:50-61
 Hash verifySigCacheKey(PublicKey const& key, Signature const& signature, ByteSlice const& bin);

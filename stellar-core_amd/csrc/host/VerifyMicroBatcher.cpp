@@ -15,13 +15,34 @@ int64_t nowNs() {
 }
 }  // namespace
 
-VerifyMicroBatcher::VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay, unsigned workers,
-                                       bool recordLatency)
-    : mMaxBatch(std::max<size_t>(1, maxBatch)), mMaxDelay(maxDelay), mRecordLatency(recordLatency) {
-  const unsigned w = std::max(1u, workers);
+VerifyMicroBatcher::VerifyMicroBatcher(Options const& o)
+    : mMaxBatch(std::max<size_t>(1, o.maxBatch)),
+      mMaxDelay(o.maxDelay),
+      mRecordLatency(o.recordLatency),
+      mPolicy(o.policy),
+      mIdleInFlight(std::max(1u, o.idleInFlight)),
+      mLinger(std::min(o.linger, o.maxDelay)) {
+  const unsigned w = std::max(1u, o.workers);
   mWorkers.reserve(w);
   for (unsigned i = 0; i < w; ++i) mWorkers.emplace_back([this] { run(); });
 }
+
+namespace {
+VerifyMicroBatcher::Options makeOptions(size_t maxBatch, std::chrono::microseconds maxDelay, unsigned workers,
+                                        bool recordLatency, VerifyMicroBatcher::FlushPolicy policy) {
+  VerifyMicroBatcher::Options o;
+  o.maxBatch = maxBatch;
+  o.maxDelay = maxDelay;
+  o.workers = workers;
+  o.recordLatency = recordLatency;
+  o.policy = policy;
+  return o;
+}
+}  // namespace
+
+VerifyMicroBatcher::VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay, unsigned workers,
+                                       bool recordLatency, FlushPolicy policy)
+    : VerifyMicroBatcher(makeOptions(maxBatch, maxDelay, workers, recordLatency, policy)) {}
 
 VerifyMicroBatcher::~VerifyMicroBatcher() {
   {
@@ -38,7 +59,7 @@ void VerifyMicroBatcher::wake() {
 }
 
 void VerifyMicroBatcher::enqueue(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg,
-                                 std::promise<bool>* done) {
+                                 std::promise<bool>* done, std::function<void(bool)>* cb) {
   // each producer thread keeps to one shard
   thread_local unsigned tShard = ~0u;
   if (tShard == ~0u) tShard = mNextShard.fetch_add(1) % kShards;
@@ -50,6 +71,7 @@ void VerifyMicroBatcher::enqueue(PublicKey const& key, ByteSlice const& sig, Byt
   std::memcpy(r.sig, sig.data(), std::min<size_t>(sig.size(), 64));
   r.msgLen = (uint32_t)msg.size();
   r.done = done;
+  r.cb = cb;
   if (mRecordLatency) r.t0 = Clock::now();
   r.arrivalNs = nowNs();
   size_t q;
@@ -63,7 +85,6 @@ void VerifyMicroBatcher::enqueue(PublicKey const& key, ByteSlice const& sig, Byt
     // the same lock) always finds it counted, so its fetch_sub never wraps
     mEnqueued.fetch_add(1);
     q = mQueued.fetch_add(1) + 1;
-    if (q == 1) mOldestNs.store(r.arrivalNs);
   }
   if (q == 1 || q == mMaxBatch) wake();
 }
@@ -81,12 +102,17 @@ int64_t VerifyMicroBatcher::oldestQueuedNs() {
 std::future<bool> VerifyMicroBatcher::submit(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg) {
   auto* p = new std::promise<bool>();
   std::future<bool> f = p->get_future();
-  enqueue(key, sig, msg, p);
+  enqueue(key, sig, msg, p, nullptr);
   return f;
 }
 
+void VerifyMicroBatcher::submit(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg,
+                                std::function<void(bool)> onVerdict) {
+  enqueue(key, sig, msg, nullptr, onVerdict ? new std::function<void(bool)>(std::move(onVerdict)) : nullptr);
+}
+
 void VerifyMicroBatcher::post(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg) {
-  enqueue(key, sig, msg, nullptr);
+  enqueue(key, sig, msg, nullptr, nullptr);
 }
 
 void VerifyMicroBatcher::drain() {
@@ -135,19 +161,40 @@ void VerifyMicroBatcher::run() {
   size_t start = 0;
   std::unique_lock<std::mutex> lk(mMu);
   for (;;) {
-    // wait for: stop, a full batch, or the oldest item's deadline
+    // wait for: stop, a full batch, an idle engine (WhenIdle) or the oldest
+    // item's deadline
     while (!mStop && mQueued.load() == 0) mCv.wait(lk);
     if (mQueued.load() == 0) return;  // stop requested and every queue drained
+    bool idle = false;
     if (mQueued.load() < mMaxBatch && !mStop) {
-      const int64_t deadline = mOldestNs.load() + (int64_t)mMaxDelay.count() * 1000;
+      // (read from the queues themselves: a count-based "first arrival" mark
+      // can lag a concurrent take)
+      const int64_t oldest = oldestQueuedNs();
+      if (oldest == INT64_MAX) {  // another worker is taking everything
+        mCv.wait_for(lk, std::chrono::microseconds(20));
+        continue;
+      }
       const int64_t now = nowNs();
-      if (now < deadline) {
-        mCv.wait_for(lk, std::chrono::nanoseconds(deadline - now),
-                     [&] { return mStop || mQueued.load() >= mMaxBatch; });
+      const int64_t deadline = oldest + (int64_t)mMaxDelay.count() * 1000;
+      const bool whenIdle = mPolicy == FlushPolicy::WhenIdle;
+      if (whenIdle && mInFlight < mIdleInFlight) {
+        const int64_t lingerEnd = oldest + (int64_t)mLinger.count() * 1000;
+        if (now < lingerEnd && now < deadline) {
+          mCv.wait_for(lk, std::chrono::nanoseconds(lingerEnd - now),
+                       [&] { return mStop || mQueued.load() >= mMaxBatch; });
+          continue;
+        }
+        idle = now < deadline;
+      } else if (now < deadline) {
+        // (WhenIdle: a completing batch notifies, and the engine is idle again)
+        mCv.wait_for(lk, std::chrono::nanoseconds(deadline - now), [&] {
+          return mStop || mQueued.load() >= mMaxBatch || (whenIdle && mInFlight < mIdleInFlight);
+        });
         continue;  // re-evaluate: another worker may have taken the queue meanwhile
       }
     }
     const bool bySize = mQueued.load() >= mMaxBatch;
+    ++mInFlight;
     lk.unlock();
     // collect up to maxBatch items, starting from a rotating shard
     size_t take = 0;
@@ -159,14 +206,10 @@ void VerifyMicroBatcher::run() {
     }
     start = (start + 1) % kShards;
     const size_t left = mQueued.fetch_sub(take) - take;
-    if (left > 0) {
-      // the leftovers keep their own deadline: the oldest one's arrival
-      const int64_t oldest = oldestQueuedNs();
-      if (oldest != INT64_MAX) mOldestNs.store(oldest);
-      if (left >= mMaxBatch) wake();
-    }
+    if (left >= mMaxBatch) wake();  // (the leftovers keep their own arrival times)
     if (take == 0) {
       lk.lock();
+      --mInFlight;
       continue;
     }
     items.clear();
@@ -186,22 +229,40 @@ void VerifyMicroBatcher::run() {
         lat.resize(take);
         for (size_t i = 0; i < take; ++i) lat[i] = std::chrono::duration<double, std::micro>(now - recs[i]->t0).count();
       }
-      for (size_t i = 0; i < take; ++i)
+      for (size_t i = 0; i < take; ++i) {
         if (std::promise<bool>* p = recs[i]->done) {
           p->set_value(v[i]);
           delete p;
         }
+        if (std::function<void(bool)>* c = recs[i]->cb) {
+          try {
+            (*c)(v[i]);
+          } catch (...) {  // (a continuation must not take the worker down)
+          }
+          delete c;
+        }
+      }
     } catch (...) {  // (only a non-ed25519 key: the reference's releaseAssert)
       ok = false;
-      for (size_t i = 0; i < take; ++i)
+      for (size_t i = 0; i < take; ++i) {
         if (std::promise<bool>* p = recs[i]->done) {
           p->set_exception(std::current_exception());
           delete p;
         }
+        if (std::function<void(bool)>* c = recs[i]->cb) {
+          try {
+            (*c)(false);
+          } catch (...) {
+          }
+          delete c;
+        }
+      }
     }
     lk.lock();
+    --mInFlight;
     ++mStats.batches;
     if (bySize) ++mStats.flushedBySize;
+    else if (idle) ++mStats.flushedIdle;
     else ++mStats.flushedByDeadline;
     mStats.items += take;
     mStats.maxBatchSeen = std::max<uint64_t>(mStats.maxBatchSeen, take);
@@ -214,6 +275,8 @@ void VerifyMicroBatcher::run() {
     }
     mCompleted += take;
     mDoneCv.notify_all();
+    // (WhenIdle: items that queued while this batch ran may flush now)
+    if (mPolicy == FlushPolicy::WhenIdle && mQueued.load() > 0) mCv.notify_all();
   }
 }
 

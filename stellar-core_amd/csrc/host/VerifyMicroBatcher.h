@@ -8,11 +8,21 @@
 // the result is only meant to warm the cache, exactly like the reference's
 // pre-verify, or submit() for a future carrying the verdict -- and a worker
 // thread flushes the queue as ONE PubKeyUtils::verifySigBatch call (which also
-// fills the cache) when it holds maxBatch items or when the oldest has waited
-// maxDelay, whichever comes first.  With workers > 1 several batches are in
-// flight at once: one worker's host work (cache walk, promise fulfilment)
-// overlaps another's engine call.  The engine and the verify cache are
-// thread-safe, so verdicts do not depend on the worker count.
+// fills the cache).  When a flush happens is the FlushPolicy:
+//   WhenIdle (default): as soon as fewer than `idleInFlight` batches are being
+//     verified, a worker flushes whatever is queued (after an optional
+//     `linger` counted from the oldest item's arrival, to let a burst that is
+//     still arriving join the batch); while batches are in flight items
+//     accumulate and are flushed when one completes, at maxBatch items, or at
+//     the oldest item's maxDelay deadline, whichever comes first.  A lone SCP
+//     envelope is verified at once (a one-item batch takes the CPU path, no GPU
+//     round trip), and under load the batches grow by themselves.
+//   Deadline: flush at maxBatch items or when the oldest has waited maxDelay
+//     (the round-2 policy: every sub-maxBatch batch pays the full maxDelay).
+// With workers > 1 several batches are in flight at once: one worker's host
+// work (cache walk, promise fulfilment) overlaps another's engine call.  The
+// engine and the verify cache are thread-safe, so verdicts do not depend on
+// the worker count or the policy.
 //
 // Queue layout: kShards sub-queues, each fixed records (key, signature
 // bytes) plus one byte arena for the messages under its own mutex; a producer
@@ -30,6 +40,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <functional>
 #include <future>
 #include <mutex>
 #include <thread>
@@ -41,10 +52,25 @@ namespace stellar {
 
 class VerifyMicroBatcher {
  public:
-  // recordLatency: keep submit -> verdict latencies of the most recent
-  // kLatencySamples items (off by default: a long-running node keeps none).
+  enum class FlushPolicy { WhenIdle, Deadline };
+  struct Options {
+    size_t maxBatch = 8192;
+    std::chrono::microseconds maxDelay{2000};
+    unsigned workers = 2;
+    // keep submit -> verdict latencies of the most recent kLatencySamples
+    // items (off by default: a long-running node keeps none)
+    bool recordLatency = false;
+    FlushPolicy policy = FlushPolicy::WhenIdle;
+    // WhenIdle: a worker flushes at once while fewer than this many batches
+    // are in flight (1: the engine's latency lane is never queued behind a
+    // second small batch of ours)
+    unsigned idleInFlight = 1;
+    // WhenIdle: an idle flush waits until the oldest item is this old
+    std::chrono::microseconds linger{0};
+  };
+  explicit VerifyMicroBatcher(Options const& opts);
   VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay, unsigned workers = 2,
-                     bool recordLatency = false);
+                     bool recordLatency = false, FlushPolicy policy = FlushPolicy::WhenIdle);
   ~VerifyMicroBatcher();  // drains the queue, then stops the workers
   VerifyMicroBatcher(VerifyMicroBatcher const&) = delete;
   VerifyMicroBatcher& operator=(VerifyMicroBatcher const&) = delete;
@@ -53,6 +79,15 @@ class VerifyMicroBatcher {
   std::future<bool> submit(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg);
   // Thread-safe, fire and forget: the verdict lands in the verify cache only.
   void post(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg);
+  // Thread-safe continuation form: onVerdict(valid) runs on a flush worker
+  // once the item's batch is verified and its verdict is IN THE VERIFY CACHE.
+  // This keeps the reference's ordering at Peer.cpp:963-979, where the
+  // overlay thread's pre-verify completes before the message is posted to the
+  // main thread: post the message from onVerdict and HerderImpl::
+  // verifyEnvelope's verifySig is a cache hit.  onVerdict must not throw and
+  // should be short (it delays the batch's other continuations); if the batch
+  // throws (a non-ed25519 key: the reference's releaseAssert) it gets false.
+  void submit(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg, std::function<void(bool)> onVerdict);
   // Blocks until every item enqueued before the call has been verified.
   void drain();
 
@@ -61,6 +96,7 @@ class VerifyMicroBatcher {
     uint64_t batches = 0;
     uint64_t flushedBySize = 0;
     uint64_t flushedByDeadline = 0;
+    uint64_t flushedIdle = 0;  // WhenIdle: below maxBatch, before the deadline, engine idle
     uint64_t maxBatchSeen = 0;
   };
   Stats stats() const;
@@ -78,6 +114,7 @@ class VerifyMicroBatcher {
     uint32_t msgLen;
     uint64_t msgOff;           // into the arena
     std::promise<bool>* done;  // submit() only
+    std::function<void(bool)>* cb;  // submit(.., onVerdict) only
     Clock::time_point t0;      // recordLatency only
     int64_t arrivalNs;         // deadline accounting (steady clock)
   };
@@ -91,7 +128,8 @@ class VerifyMicroBatcher {
     std::mutex mu;
     Queue q;
   };
-  void enqueue(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg, std::promise<bool>* done);
+  void enqueue(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg, std::promise<bool>* done,
+               std::function<void(bool)>* cb);
   void wake();
   // moves up to `want` of the oldest items of shard s into `into`; returns the count
   size_t takeFrom(size_t s, size_t want, Queue& into);
@@ -100,9 +138,12 @@ class VerifyMicroBatcher {
   const size_t mMaxBatch;
   const std::chrono::microseconds mMaxDelay;
   const bool mRecordLatency;
+  const FlushPolicy mPolicy;
+  const unsigned mIdleInFlight;
+  const std::chrono::microseconds mLinger;
+  unsigned mInFlight = 0;  // batches being verified (under mMu)
   Shard mShards[kShards];
   std::atomic<size_t> mQueued{0};
-  std::atomic<int64_t> mOldestNs{0};   // arrival (steady_clock ns) of the oldest queued item
   std::atomic<uint64_t> mEnqueued{0};
   std::atomic<unsigned> mNextShard{0};
   mutable std::mutex mMu;  // worker wake-ups, stats, drain

@@ -4,6 +4,7 @@
 // boundary.
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -358,8 +359,10 @@ int svh_mb_run_ex(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, con
     if (workers < 1) workers = 1;
     std::vector<int> err(producers, 0);
     std::vector<std::string> msgs(producers);
+    // (the round-2 deadline policy: these entry points' callers and tests
+    // count size and deadline flushes; svh_scp_run drives the WhenIdle default)
     VerifyMicroBatcher mb(max_batch, std::chrono::microseconds(max_delay_us), (unsigned)workers,
-                          /*recordLatency=*/!fire_and_forget);
+                          /*recordLatency=*/!fire_and_forget, VerifyMicroBatcher::FlushPolicy::Deadline);
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int p = 0; p < producers; ++p) {
@@ -415,6 +418,140 @@ int svh_mb_run_ex(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, con
       stats->lat_p99_us = lat.empty() ? 0 : lat[std::min(lat.size() - 1, (size_t)(lat.size() * 0.99))];
       stats->wall_s = wall;
     }
+    return SVH_OK;
+  } catch (std::exception const& e) {
+    return guard_exc(e);
+  }
+}
+
+int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
+                const uint32_t* msg_len, size_t n, const svh_scp_params* prm, uint8_t* verdict, svh_scp_result* res) {
+  try {
+    if (!prm || !res || prm->struct_size < sizeof(svh_scp_params) || n == 0 || !pk || !sig || !msg_off ||
+        !msg_len)
+      throw std::invalid_argument("svh_scp_run: bad arguments");
+    using Clk = std::chrono::steady_clock;
+    const unsigned P = std::max(1u, prm->producers);
+    const size_t B = prm->burst ? prm->burst : n;
+    VerifyMicroBatcher::Options o;
+    o.maxBatch = prm->max_batch ? prm->max_batch : 8192;
+    o.maxDelay = std::chrono::microseconds(prm->max_delay_us);
+    o.workers = std::max(1u, prm->workers);
+    o.policy = prm->policy == 1 ? VerifyMicroBatcher::FlushPolicy::Deadline : VerifyMicroBatcher::FlushPolicy::WhenIdle;
+    o.idleInFlight = std::max(1u, prm->idle_in_flight);
+    o.linger = std::chrono::microseconds(prm->linger_us);
+    std::vector<Clk::time_point> tSub(n), tVer(n), tMain(n);
+    std::vector<uint8_t> cbVerdict(n, 2);
+    // the main thread's queue (Peer::recvMessage posted by the continuation)
+    std::mutex qm;
+    std::condition_variable qcv;
+    std::vector<size_t> q;
+    q.reserve(n);
+    (void)PubKeyUtils::flushEngineCounts();  // (the run's own counts are read at the end)
+    std::vector<uint8_t> out(n, 2);
+    uint64_t hits = 0, misses = 0, mismatches = 0;
+    std::vector<double> mainCallUs;
+    mainCallUs.reserve(n);
+    const Clk::time_point T0 = Clk::now() + std::chrono::milliseconds(2);
+    VerifyMicroBatcher::Stats st;
+    {
+      VerifyMicroBatcher mb(o);
+      // the main thread: HerderImpl::verifyEnvelope per envelope, in the order
+      // the continuations posted them (HerderImpl.cpp:2414-2432)
+      std::thread mainThr([&] {
+        uint64_t h0, m0;
+        PubKeyUtils::flushThreadVerifySigCounts(h0, m0);
+        size_t doneN = 0, head = 0;
+        std::vector<size_t> local;
+        while (doneN < n) {
+          {
+            std::unique_lock<std::mutex> lk(qm);
+            qcv.wait(lk, [&] { return q.size() > head; });
+            local.assign(q.begin() + (ptrdiff_t)head, q.end());
+            head = q.size();
+          }
+          for (size_t i : local) {
+            PublicKey k;
+            std::memcpy(k.ed25519().data(), pk + 32 * i, 32);
+            Signature s(sig + 64 * i, sig + 64 * i + 64);
+            const auto a = Clk::now();
+            const bool v = PubKeyUtils::verifySig(k, s, ByteSlice(msg + msg_off[i], msg_len[i]));
+            const auto b = Clk::now();
+            tMain[i] = b;
+            mainCallUs.push_back(std::chrono::duration<double, std::micro>(b - a).count());
+            out[i] = v ? 1 : 0;
+            if ((uint8_t)v != cbVerdict[i]) ++mismatches;
+            ++doneN;
+          }
+        }
+        PubKeyUtils::flushThreadVerifySigCounts(hits, misses);
+      });
+      std::vector<std::thread> th;
+      for (unsigned p = 0; p < P; ++p) {
+        th.emplace_back([&, p] {
+          PublicKey k;
+          for (size_t b0 = 0, burst = 0; b0 < n; b0 += B, ++burst) {
+            if (prm->interval_us) std::this_thread::sleep_until(T0 + std::chrono::microseconds((uint64_t)prm->interval_us * burst));
+            const size_t b1 = std::min(n, b0 + B);
+            for (size_t i = b0 + p; i < b1; i += P) {
+              std::memcpy(k.ed25519().data(), pk + 32 * i, 32);
+              tSub[i] = Clk::now();
+              mb.submit(k, ByteSlice(sig + 64 * i, 64), ByteSlice(msg + msg_off[i], msg_len[i]), [&, i](bool v) {
+                tVer[i] = Clk::now();
+                cbVerdict[i] = v ? 1 : 0;
+                {
+                  std::lock_guard<std::mutex> g(qm);
+                  q.push_back(i);
+                }
+                qcv.notify_one();
+              });
+            }
+          }
+        });
+      }
+      for (auto& t : th) t.join();
+      mainThr.join();
+      mb.drain();
+      st = mb.stats();
+    }
+    auto eng = PubKeyUtils::flushEngineCounts();
+    std::vector<double> lv(n), lm(n);
+    Clk::time_point first = tSub[0], last = tMain[0];
+    for (size_t i = 0; i < n; ++i) {
+      lv[i] = std::chrono::duration<double, std::micro>(tVer[i] - tSub[i]).count();
+      lm[i] = std::chrono::duration<double, std::micro>(tMain[i] - tSub[i]).count();
+      first = std::min(first, tSub[i]);
+      last = std::max(last, tMain[i]);
+    }
+    auto pct = [](std::vector<double> v, double q) {
+      std::sort(v.begin(), v.end());
+      return v[std::min(v.size() - 1, (size_t)(q * (double)v.size()))];
+    };
+    double mean = 0;
+    for (double x : lv) mean += x;
+    res->verdict_p50_us = pct(lv, 0.5);
+    res->verdict_p90_us = pct(lv, 0.9);
+    res->verdict_p99_us = pct(lv, 0.99);
+    res->verdict_max_us = pct(lv, 1.0);
+    res->verdict_mean_us = mean / (double)n;
+    res->main_p50_us = pct(lm, 0.5);
+    res->main_p99_us = pct(lm, 0.99);
+    res->main_call_p50_us = pct(mainCallUs, 0.5);
+    res->main_hits = hits;
+    res->main_misses = misses;
+    res->main_mismatches = mismatches;
+    res->batches = st.batches;
+    res->flushed_by_size = st.flushedBySize;
+    res->flushed_by_deadline = st.flushedByDeadline;
+    res->flushed_idle = st.flushedIdle;
+    res->max_batch = st.maxBatchSeen;
+    res->mean_batch = st.batches ? (double)st.items / (double)st.batches : 0;
+    res->gpu_batches = eng.gpuBatches;
+    res->gpu_signatures = eng.gpuSignatures;
+    res->cpu_signatures = eng.cpuSignatures;
+    res->fallbacks = eng.fallbacks;
+    res->wall_s = std::chrono::duration<double>(last - first).count();
+    if (verdict) std::memcpy(verdict, out.data(), n);
     return SVH_OK;
   } catch (std::exception const& e) {
     return guard_exc(e);

@@ -196,7 +196,8 @@ struct LatLane {
   hipStream_t build = nullptr;   // key-table builds (lowest priority)
   hipEvent_t ev_lat = nullptr, done = nullptr, keys_down = nullptr;
   HostBuf h_in, h_out, h_build;
-  HostBuf z_out;  // mapped: the kernels write verdicts in place
+  HostBuf z_out;   // mapped: the kernels write verdicts in place
+  HostBuf z_keys;  // mapped: the hash kernel writes cache keys in place (keyed batches)
   DevBuf d_in, d_out, d_keys, d_build;
   void* ctab = nullptr;  // tables of B (built at lane init)
   DevBuf ktab, kstat;    // tables of -A per cached key, status per slot
@@ -805,6 +806,11 @@ std::vector<size_t> key_pieces(size_t m) {
 // k's events have been recorded (recorded(k + 1)); join() returns the first
 // error.  The destructor stops and joins it (an early error return of the
 // caller).
+// Depth of engine entry points on this thread (LifeGuard below); > 0 also on a
+// KeyNotifier thread, whose callbacks run inside the caller's entry point, so
+// sv_shutdown / sv_set_device_map from a callback is refused there too.
+thread_local int t_life_depth = 0;
+
 class KeyNotifier {
  public:
   ~KeyNotifier() {
@@ -814,6 +820,8 @@ class KeyNotifier {
   void start(int dev, size_t P, std::function<int(size_t)> fn) {
     fn_ = std::move(fn);
     th_ = std::thread([this, dev, P] {
+      // (the caller holds the lifetime lock until this thread is joined)
+      t_life_depth = 1;
       (void)hipSetDevice(dev);
       for (size_t k = 0; k < P; ++k) {
         while (rec_.load(std::memory_order_acquire) <= k) {
@@ -1103,6 +1111,7 @@ void release_lat(LatLane& L) {
   L.pending_n.clear();
   L.h_in.release(); L.h_out.release(); L.h_build.release();
   L.z_out.release();
+  L.z_keys.release();
   L.d_in.release(); L.d_out.release(); L.d_keys.release(); L.d_build.release();
   L.ktab.release(); L.kstat.release();
   if (L.ctab) (void)hipFree(L.ctab);
@@ -1134,6 +1143,7 @@ int lat_ready(Device& D) {
   SV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   SV_HIP(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, greatest));
   L.z_out.mapped = true;
+  L.z_keys.mapped = true;
   L.h_in.mapped = true;  // (the kernels read it in place: lat_in_place)
   L.ready = true;  // (release_lat cleans up whatever exists from here on)
   hipError_t e = hipStreamCreateWithPriority(&L.build, hipStreamNonBlocking, least);
@@ -1367,17 +1377,18 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   const Image im = image_of(in, 0, n, &msg_total);
   const size_t o_ks = (im.bytes + 3) & ~(size_t)3;
   const size_t in_bytes = warm ? o_ks + 4 * n : im.bytes;
-  const size_t out_per = (verdict ? 1 : 0) + (keys ? 32 : 0);
-  const bool zc = verdict && !keys && lat_zero_copy();
+  // zero-copy outputs: verdicts (and a keyed batch's cache keys) written by
+  // the kernels straight into mapped pinned memory, no D2H blit
+  const bool zc = verdict && lat_zero_copy();
+  const bool zk = keys && lat_zero_copy();
+  const size_t out_per = (verdict && !zc ? 1 : 0) + (keys && !zk ? 32 : 0);
   const bool in_place = lat_in_place();
   if ((rc = L.h_in.ensure(in_bytes)) || (!in_place && (rc = L.d_in.ensure(in_bytes)))) return rc;
-  if (zc) {
-    if ((rc = L.z_out.ensure(n))) return rc;
-  } else {
-    if ((rc = L.h_out.ensure(out_per * n))) return rc;
-    if (verdict && (rc = L.d_out.ensure(n))) return rc;
-    if (keys && (rc = L.d_keys.ensure(32 * n))) return rc;
-  }
+  if (zc && (rc = L.z_out.ensure(n))) return rc;
+  if (zk && (rc = L.z_keys.ensure(32 * n))) return rc;
+  if (out_per && (rc = L.h_out.ensure(out_per * n))) return rc;
+  if (verdict && !zc && (rc = L.d_out.ensure(n))) return rc;
+  if (keys && !zk && (rc = L.d_keys.ensure(32 * n))) return rc;
   uint8_t* h = (uint8_t*)L.h_in.p;
   pack(in, 0, n, im, h);
   if (warm) std::memcpy(h + o_ks, L.kslots.data(), 4 * n);
@@ -1386,16 +1397,19 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   const auto t_up = std::chrono::steady_clock::now();
   uint8_t* d = (uint8_t*)(in_place ? L.h_in.dp : L.d_in.p);
   void* d_verdict = zc ? L.z_out.dp : L.d_out.p;
+  void* d_keys = zk ? L.z_keys.dp : L.d_keys.p;
   const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
   const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
   uint8_t* ho = (uint8_t*)L.h_out.p;
+  const uint8_t* vho = zc ? (const uint8_t*)L.z_out.p : ho;  // verdicts on the host
+  uint8_t* kho = zk ? (uint8_t*)L.z_keys.p : ho + (verdict && !zc ? n : 0);  // keys on the host
   const bool early = kcb && keys && verdict;
   auto t_k = t_up;
   if (keys) {
-    SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n, L.d_keys.p,
+    SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n, d_keys,
                           L.stream));
     if (early) {
-      SV_HIP(hipMemcpyAsync(ho + n, L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, L.stream));
+      if (!zk) SV_HIP(hipMemcpyAsync(kho, L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, L.stream));
       SV_HIP(hipEventRecord(L.keys_down, L.stream));
     }
   }
@@ -1417,21 +1431,20 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
     t_k = std::chrono::steady_clock::now();
     if (!zc) SV_HIP(hipMemcpyAsync(ho, L.d_out.p, n, hipMemcpyDeviceToHost, L.stream));
   }
-  if (keys && !early)
-    SV_HIP(hipMemcpyAsync(ho + (verdict ? n : 0), L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, L.stream));
+  if (keys && !early && !zk) SV_HIP(hipMemcpyAsync(kho, L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, L.stream));
   SV_HIP(hipEventRecord(L.done, L.stream));
   const auto t_down = std::chrono::steady_clock::now();
   if (early) {
     SV_HIP(hipEventSynchronize(L.keys_down));
-    std::memcpy(keys, ho + n, 32 * n);
+    std::memcpy(keys, kho, 32 * n);
     kcb(n);
     *cb_done = true;
   }
   lat_build(L);  // (after the verify work: a build waits for it on the device)
   const auto t_b = std::chrono::steady_clock::now();
   SV_HIP(hipEventSynchronize(L.done));
-  if (verdict) std::memcpy(verdict, zc ? (const uint8_t*)L.z_out.p : ho, n);
-  if (keys && !early) std::memcpy(keys, ho + (verdict ? n : 0), 32 * n);
+  if (verdict) std::memcpy(verdict, vho, n);
+  if (keys && !early) std::memcpy(keys, kho, 32 * n);
   if (warm) ++L.warm;
   else ++L.cold;
   const auto t2 = std::chrono::steady_clock::now();
@@ -1660,7 +1673,6 @@ class LifeLock {
   bool writer_ = false;
 };
 LifeLock g_life;
-thread_local int t_life_depth = 0;
 struct LifeGuard {
   LifeGuard() {
     if (t_life_depth++ == 0) g_life.lock_shared();
@@ -1684,7 +1696,10 @@ extern "C" {
 int sv_init(void) { return ensure_init(); }
 
 void sv_shutdown(void) {
-  if (t_life_depth != 0) return;  // (from inside an engine call, e.g. a keys-ready callback: refused)
+  if (t_life_depth != 0) {  // (from inside an engine call, e.g. a keys-ready callback: refused)
+    (void)fail(SV_ERR_INVALID_ARG, "sv_shutdown called from inside an engine call: refused");
+    return;
+  }
   std::unique_lock<LifeLock> life(g_life);  // waits for every in-flight call
   std::lock_guard<std::mutex> g(g_mu);
   shutdown_locked();

@@ -512,7 +512,9 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
 #define SV_OCTET_LDS_BYTES(MSG) (SV_OCTET_TAB_BYTES + ((MSG) ? SV_OSIGS * SV_MSG_CAP : 0))
 template <int MODE, bool MSG>
 __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams p) {
-  extern __shared__ uint32_t s_dyn[];
+  // (16-byte aligned: the tables and the message windows are read as sv_u4)
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+  static_assert(SV_OCTET_TAB_BYTES % 16 == 0, "the message windows follow the tables at a 16-byte boundary");
   uint32_t(*s_tab)[2][SV_ATAB_ENTRIES][SV_QENT_DW] = (uint32_t(*)[2][SV_ATAB_ENTRIES][SV_QENT_DW])s_dyn;
   __builtin_amdgcn_s_setprio(3);  // latency class (as sv_comb_kernel)
   const uint32_t lane = threadIdx.x & 63u;

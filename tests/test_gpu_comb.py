@@ -13,7 +13,11 @@ keys for a table build.  Both must give libsodium's verdict on every row:
   * eviction: a cache smaller than the key set still gives exact verdicts;
   * the staged-copy lane (SV_LAT_ZC_IN=0 / SV_LAT_ZERO_COPY=0: one H2D of the
     image, one D2H of the verdicts) gives the same verdicts as the default
-    (kernels read the image and write the verdicts in mapped memory).
+    (kernels read the image and write the verdicts in mapped memory);
+  * the same staged fallbacks for keyed lane batches (keys D2H instead of
+    written in mapped memory) and for one-chunk bulk batches (SV_BULK_ZC_IN=0:
+    staged H2D instead of the image read in place), keyed, unkeyed and through
+    the pieced progress path, verdicts and BLAKE2b keys exact.
 """
 import os
 import subprocess
@@ -216,3 +220,92 @@ def test_staged_copy_lane_matches(sv, gpu, oracle, tmp_path):
     outs = np.load(dst, allow_pickle=False)
     for it, out in enumerate(outs):
         assert (out == d["verdict"]).all(), (it, np.nonzero(out != d["verdict"])[0][:10])
+
+
+_STAGED_KEYED_CHILD = r"""
+import ctypes, os, sys
+import numpy as np
+import torch  # noqa: F401  (the HIP runtime torch ships, as in the parent)
+z = np.load(sys.argv[2], allow_pickle=False)
+lib = ctypes.CDLL(os.path.join(sys.argv[1], "stellar-core_amd", "libstellar_sigverify.so"))
+class Opts(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32), ("max_devices", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+vp = ctypes.c_void_p
+arrs = [np.ascontiguousarray(z[k]) for k in ("pk", "sig", "msg", "msg_off", "msg_len")]
+n = len(arrs[4])
+assert lib.sv_init() == 0
+res = {}
+for name, flags in (("lane", 0x2), ("bulk", 0x1)):
+    opts = Opts(ctypes.sizeof(Opts), 0, 0, flags)
+    for it in range(3):
+        out = np.zeros(n, np.uint8)
+        keys = np.zeros((n, 32), np.uint8)
+        rc = lib.sv_ed25519_verify_batch_keyed(*[vp(a.ctypes.data) for a in arrs], ctypes.c_size_t(n),
+                                               vp(out.ctypes.data), vp(keys.ctypes.data), ctypes.byref(opts))
+        assert rc == 0, rc
+        res["%s_keyed_%d_v" % (name, it)] = out
+        res["%s_keyed_%d_k" % (name, it)] = keys
+        out = np.zeros(n, np.uint8)
+        rc = lib.sv_ed25519_verify_batch(*[vp(a.ctypes.data) for a in arrs], ctypes.c_size_t(n),
+                                         vp(out.ctypes.data), ctypes.byref(opts))
+        assert rc == 0, rc
+        res["%s_plain_%d_v" % (name, it)] = out
+# the pieced progress path: a one-chunk keyed bulk batch with a keys-ready
+# callback (keys come back in pieces while the GPU verifies), 12x the set
+reps = 12
+m = n * reps
+msg = arrs[2]
+P = lambda a, stride, k: (ctypes.c_void_p * m)(*[a.ctypes.data + stride * (i % n) for i in range(m)])
+ppk, psig = P(arrs[0], 32, 0), P(arrs[1], 64, 0)
+pmsg = (ctypes.c_void_p * m)(*[msg.ctypes.data + int(arrs[3][i % n]) for i in range(m)])
+plen = np.ascontiguousarray(np.tile(arrs[4], reps))
+seen = []
+CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_size_t)
+cb = CB(lambda ctx, ready: seen.append(ready))
+out = np.zeros(m, np.uint8)
+keys = np.zeros((m, 32), np.uint8)
+opts = Opts(ctypes.sizeof(Opts), 0, 0, 0x1)
+rc = lib.sv_ed25519_verify_batch_gather_progress(ppk, psig, pmsg, vp(plen.ctypes.data), ctypes.c_size_t(m),
+                                                  vp(out.ctypes.data), vp(keys.ctypes.data), cb, None,
+                                                  ctypes.byref(opts))
+assert rc == 0, rc
+assert seen and seen[-1] == m and seen == sorted(seen), seen
+res["pieced_pieces"] = np.array([len(seen)])
+res["pieced_v"] = out
+res["pieced_k"] = keys
+np.savez(sys.argv[3], **res)
+"""
+
+
+def test_staged_fallbacks_keyed_and_bulk(sv, gpu, oracle, tmp_path):
+    """SV_LAT_ZC_IN=0, SV_LAT_ZERO_COPY=0 and SV_BULK_ZC_IN=0 (the staged
+    fallbacks; env switches are read once per process, hence a child): keyed
+    and unkeyed lane and one-chunk bulk batches, and the pieced progress path,
+    against the oracle's verdicts and hashlib's BLAKE2b-256 keys."""
+    import hashlib
+    d = _scp_set(oracle, 1000, seed=78)
+    src = tmp_path / "set.npz"
+    np.savez(src, pk=d["pk"], sig=d["sig"], msg=d["msg"], msg_off=d["msg_off"].astype(np.uint64),
+             msg_len=d["msg_len"].astype(np.uint32))
+    dst = tmp_path / "out.npz"
+    env = dict(os.environ, SV_LAT_ZC_IN="0", SV_LAT_ZERO_COPY="0", SV_BULK_ZC_IN="0")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _STAGED_KEYED_CHILD, repo, str(src), str(dst)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = dict(np.load(dst, allow_pickle=False))
+    n = len(d["verdict"])
+    want_k = np.zeros((n, 32), np.uint8)
+    for i in range(n):
+        o, ln = int(d["msg_off"][i]), int(d["msg_len"][i])
+        want_k[i] = np.frombuffer(hashlib.blake2b(d["pk"][i].tobytes() + d["sig"][i].tobytes()
+                                                  + d["msg"][o:o + ln].tobytes(), digest_size=32).digest(), np.uint8)
+    for k, v in res.items():
+        if k.endswith("_v"):
+            reps = len(v) // n
+            assert (v == np.tile(d["verdict"], reps)).all(), k
+        elif k.endswith("_k"):
+            reps = len(v) // n
+            assert (v == np.tile(want_k, (reps, 1))).all(), k
+    assert res["pieced_pieces"][0] >= 2

@@ -5,9 +5,10 @@ bulk launches made while latency batches are live run in shared mode (a
 workgroup slot per CU left free, csrc/sv_kernels.hip sv_launch_verify) and the
 latency lane has its own high-priority stream, staging and mutex
 (csrc/sv_api.cpp LatLane).  The 1k batches' p99 under load is recorded
-(SV_ISOLATION_OUT, profiles/) as evidence, not asserted: wall-clock thresholds
-belong to the bench, not to the correctness suite (SV_ISOLATION_P99_MS=x opts
-in to a bound)."""
+(SV_ISOLATION_OUT, profiles/) and held to a loose bound, 1 ms by default
+(SV_ISOLATION_P99_MS=x overrides): the round-4 runs measured 0.21-0.23 ms; a
+lane copy queued behind bulk uploads again (0.6-0.86 ms before round 4) comes
+close to it, the multi-ms stalls of an unisolated lane do not pass."""
 import json
 import os
 
@@ -33,6 +34,5 @@ def test_latency_batches_under_bulk_load(sv, oracle):
     assert res["shared_launches"] > 0
     during = res["latency_during_bulk"]
     assert during["batches"] >= 100, res
-    bound = os.environ.get("SV_ISOLATION_P99_MS")
-    if bound:
-        assert during["p99_ms"] <= float(bound), res
+    bound = float(os.environ.get("SV_ISOLATION_P99_MS", "1.0"))
+    assert during["p99_ms"] <= bound, res

@@ -38,6 +38,7 @@ def host(sv):
     lib.svh_set_cpu_threshold.argtypes = [ctypes.c_size_t]
     lib.svh_cache_keys.restype = ctypes.c_size_t
     lib.svh_cache_seed.argtypes = [ctypes.c_uint]
+    lib.svh_scp_run.restype = ctypes.c_int
     return lib
 
 
@@ -487,6 +488,103 @@ def test_micro_batcher_multiple_workers(host, engine, golden):
     out, st = _mb_run(host, d, rows, producers=1, max_batch=1000, max_delay_us=3000, gap_us=500, workers=3)
     assert (out == 1).all()
     assert st.flushed_by_size == 0 and st.flushed_by_deadline >= 1 and st.items == 6
+
+
+class ScpParams(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint32) for k in ("struct_size", "producers", "burst", "interval_us", "max_batch",
+                                               "max_delay_us", "workers", "policy", "linger_us", "idle_in_flight")]
+
+
+class ScpResult(ctypes.Structure):
+    _fields_ = ([(k, ctypes.c_double) for k in ("verdict_p50_us", "verdict_p90_us", "verdict_p99_us",
+                                                "verdict_max_us", "verdict_mean_us", "main_p50_us", "main_p99_us",
+                                                "main_call_p50_us")]
+                + [(k, ctypes.c_uint64) for k in ("main_hits", "main_misses", "main_mismatches", "batches",
+                                                  "flushed_by_size", "flushed_by_deadline", "flushed_idle",
+                                                  "max_batch")]
+                + [("mean_batch", ctypes.c_double)]
+                + [(k, ctypes.c_uint64) for k in ("gpu_batches", "gpu_signatures", "cpu_signatures", "fallbacks")]
+                + [("wall_s", ctypes.c_double)])
+
+
+def scp_run(host, d, rows, producers, burst, interval_us, max_batch=8192, max_delay_us=2000, workers=2, policy=0,
+            linger_us=0):
+    """svh_scp_run (config 4 through the micro-batcher: continuation submits,
+    a main thread calling verifySig per envelope) over golden rows."""
+    n = len(rows)
+    pk = np.ascontiguousarray(d["pk"][rows])
+    sig = np.ascontiguousarray(d["sig"][rows])
+    off = np.ascontiguousarray(d["msg_off"][rows])
+    ln = np.ascontiguousarray(d["msg_len"][rows])
+    msg = np.ascontiguousarray(d["msg"])
+    out = np.full(n, 7, np.uint8)
+    p = ScpParams(ctypes.sizeof(ScpParams), producers, burst, interval_us, max_batch, max_delay_us, workers, policy,
+                  linger_us, 1)
+    r = ScpResult()
+    vp = ctypes.c_void_p
+    rc = host.svh_scp_run(vp(pk.ctypes.data), vp(sig.ctypes.data), vp(msg.ctypes.data), vp(off.ctypes.data),
+                          vp(ln.ctypes.data), ctypes.c_size_t(n), ctypes.byref(p), vp(out.ctypes.data),
+                          ctypes.byref(r))
+    assert rc == 0, host.svh_last_error_string()
+    return out, r
+
+
+def test_scp_run_idle_flush_trickle(host, engine, golden):
+    """WhenIdle policy (VerifyMicroBatcher.h): a trickle of lone envelopes is
+    flushed as each arrives -- no batch waits out maxDelay (200 ms here) --
+    every continuation precedes the main thread's verifySig, which hits the
+    cache (the Peer.cpp:963-979 -> HerderImpl.cpp:2414-2432 order)."""
+    d = golden["adversarial"]
+    rows = np.arange(0, len(d["verdict"]), 7)[:24]
+    out, r = scp_run(host, d, rows, producers=1, burst=1, interval_us=3000, max_delay_us=200_000)
+    assert (out == d["verdict"][rows]).all()
+    assert r.main_hits == len(rows) and r.main_misses == 0 and r.main_mismatches == 0
+    assert r.flushed_idle == r.batches and r.flushed_by_deadline == 0 and r.flushed_by_size == 0
+    assert r.verdict_max_us < 100_000  # (far below the 200 ms deadline)
+
+
+def test_scp_run_bursts_many_producers(host, engine, golden):
+    """Bursts from several producers under WhenIdle: batches grow while one is
+    in flight; every item's verdict and the main thread's hit are exact.
+    (Distinct envelopes: a duplicate in flight in two batches is pending under
+    the later one until it resolves, and a verifySig meanwhile is a miss, as
+    for concurrent verifySig calls; the overlay drops duplicates before the
+    pre-verify, Peer.cpp:957-960.)"""
+    d = golden["adversarial"]
+    seen, rows = set(), []
+    for i in range(len(d["verdict"])):
+        o, ln = int(d["msg_off"][i]), int(d["msg_len"][i])
+        k = d["pk"][i].tobytes() + d["sig"][i].tobytes() + d["msg"][o:o + ln].tobytes()
+        if k not in seen:
+            seen.add(k)
+            rows.append(i)
+    rows = np.array(rows)
+    out, r = scp_run(host, d, rows, producers=4, burst=64, interval_us=20_000, max_delay_us=500_000)
+    assert (out == d["verdict"][rows]).all()
+    assert r.main_hits == len(rows) and r.main_mismatches == 0
+    assert r.batches == r.flushed_by_size + r.flushed_by_deadline + r.flushed_idle
+    assert r.flushed_idle >= 1 and r.max_batch <= 8192
+
+
+def test_scp_run_deadline_policy_waits(host, engine, golden):
+    """The round-2 Deadline policy, for contrast: a lone envelope waits out
+    maxDelay before its batch is flushed."""
+    d = golden["valid"]
+    rows = np.arange(6)
+    out, r = scp_run(host, d, rows, producers=1, burst=1, interval_us=20_000, max_delay_us=5000, policy=1)
+    assert (out == 1).all() and r.main_hits == len(rows)
+    assert r.flushed_idle == 0 and r.flushed_by_deadline == r.batches
+    assert r.verdict_p50_us >= 4900
+
+
+def test_scp_run_linger_collects_a_burst(host, engine, golden):
+    """linger: an idle flush waits until the oldest item is that old, so a
+    burst that arrives within it becomes one batch."""
+    d = golden["valid"]
+    rows = np.arange(32)
+    out, r = scp_run(host, d, rows, producers=1, burst=32, interval_us=0, max_delay_us=400_000, linger_us=200_000)
+    assert (out == 1).all() and r.main_hits == len(rows)
+    assert r.batches == 1 and r.max_batch == 32
 
 
 @pytest.mark.gpu
