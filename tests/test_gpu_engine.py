@@ -318,6 +318,40 @@ def test_micro_batcher_through_engine(sv, dev, golden, post):
     host.svh_cache_clear()
 
 
+@pytest.mark.parametrize("burst,interval_us,linger_us", [(500, 2000, 0), (4, 100, 0), (0, 0, 0), (500, 2000, 50)])
+def test_scp_integrated_path(sv, dev, golden, burst, interval_us, linger_us):
+    """Config 4 through the integration path on the GPU (svh_scp_run): overlay
+    producers -> VerifyMicroBatcher (WhenIdle) -> keyed verifySigBatch (GPU
+    BLAKE2b keys, mapped keys / verdicts on the latency lane) -> continuation
+    -> main-thread verifySig.  Distinct adversarial + 0..512 B rows: every
+    verdict equals libsodium's, every main-thread call is a cache hit."""
+    from test_host_mirror import scp_run
+    host = _host(sv)
+    host.svh_scp_run.restype = ctypes.c_int
+    parts = [golden["adversarial"], golden["msglen"]]
+    d = {"pk": np.concatenate([p["pk"] for p in parts]), "sig": np.concatenate([p["sig"] for p in parts]),
+         "verdict": np.concatenate([p["verdict"] for p in parts]),
+         "msg": np.concatenate([p["msg"] for p in parts]),
+         "msg_off": np.concatenate([parts[0]["msg_off"], parts[1]["msg_off"] + len(parts[0]["msg"])]),
+         "msg_len": np.concatenate([p["msg_len"] for p in parts])}
+    seen, rows = set(), []
+    for i in range(len(d["verdict"])):
+        o, ln = int(d["msg_off"][i]), int(d["msg_len"][i])
+        k = d["pk"][i].tobytes() + d["sig"][i].tobytes() + d["msg"][o:o + ln].tobytes()
+        if k not in seen:
+            seen.add(k)
+            rows.append(i)
+    rows = np.array(rows)
+    host.svh_cache_clear()
+    _stats(host)
+    out, r = scp_run(host, d, rows, producers=4, burst=burst, interval_us=interval_us, linger_us=linger_us)
+    assert np.array_equal(out, d["verdict"][rows])
+    assert r.main_hits == len(rows) and r.main_misses == 0 and r.main_mismatches == 0
+    assert r.fallbacks == 0 and r.gpu_batches >= 1
+    assert r.batches == r.flushed_by_size + r.flushed_by_deadline + r.flushed_idle
+    host.svh_cache_clear()
+
+
 # ------------------------------------------------ catchup prefetch (f3)
 def test_checkpoint_prefetch_1m_signatures(sv, dev):
     """one checkpoint's worth of envelopes (2^20 single-signature
