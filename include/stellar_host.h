@@ -132,6 +132,11 @@ void svh_set_keyed_threshold(size_t min_items);
  * the checkers looking their pairs up in the table only */
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs);
+/* Wall-clock phases (ms) of the calling thread's last svh_check_txset:
+ * [0] C structs -> the mirror's objects, [1] pair enumeration (prefetch add),
+ * [2] the engine pre-pass (prefetch run: one GPU batch + side table),
+ * [3] the checkers.  [1] and [2] are 0 without the pre-pass. */
+void svh_txset_last_phases(double out[4]);
 
 /* ---- transaction-level checks (a13) ---- */
 typedef struct svh_account {

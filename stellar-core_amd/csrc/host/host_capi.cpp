@@ -33,13 +33,17 @@ namespace {
 const bool gPhaseTrace = getenv("SV_HOST_TRACE") != nullptr;
 struct PhaseClock {
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-  void lap(const char* what) {
-    if (!gPhaseTrace) return;
+  // returns the lap in ms
+  double lap(const char* what) {
     const auto now = std::chrono::steady_clock::now();
-    fprintf(stderr, "[svh] %-28s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+    const double ms = std::chrono::duration<double, std::milli>(now - t).count();
+    if (gPhaseTrace) fprintf(stderr, "[svh] %-28s %8.3f ms\n", what, ms);
     t = now;
+    return ms;
   }
 };
+// phases of this thread's last svh_check_txset (svh_txset_last_phases)
+thread_local double t_txset_phases[4] = {0, 0, 0, 0};
 thread_local std::string t_err;
 int guard_exc(std::exception const& e) {
   t_err = e.what();
@@ -252,15 +256,16 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
         for (uint32_t k = 0; k < txs[t].nsigners; ++k) sgn[t].push_back(signer(signers[txs[t].signer_off + k]));
       }
     });
-    pc.lap("txset: marshal");
+    double ph[4] = {0, 0, 0, 0};
+    ph[0] = pc.lap("txset: marshal");
     SignatureBatchPrefetch pre;
     if (use_prefetch) {
       std::vector<SignatureBatchPrefetch::TxRef> refs(ntx);
       for (size_t t = 0; t < ntx; ++t) refs[t] = {&hashes[t], &dsigs[t], &sgn[t]};
       pre.addBatch(refs);
-      pc.lap("txset: prefetch add");
+      ph[1] = pc.lap("txset: prefetch add");
       pre.run(use_prefetch == 2);
-      pc.lap("txset: prefetch run");
+      ph[2] = pc.lap("txset: prefetch run");
     }
     if (prefetched_pairs) *prefetched_pairs = pre.pairs();
     auto check = [&](size_t a, size_t b) {
@@ -276,12 +281,15 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
     // flow: one verifySig per signature) they run in tx order on this thread.
     if (use_prefetch) parallelOrThrow(ntx, 128, check);
     else check(0, ntx);
-    pc.lap("txset: checkers");
+    ph[3] = pc.lap("txset: checkers");
+    std::memcpy(t_txset_phases, ph, sizeof ph);
     return SVH_OK;
   } catch (std::exception const& e) {
     return guard_exc(e);
   }
 }
+
+void svh_txset_last_phases(double out[4]) { std::memcpy(out, t_txset_phases, sizeof t_txset_phases); }
 
 int svh_check_envelopes(const svh_envelope* env, size_t n, const svh_decorated_sig* sigs, const svh_op* ops,
                         const svh_signer* signers, const svh_account* accounts, size_t naccounts,

@@ -289,22 +289,35 @@ def config3(env, n_tx=5000, sets=5):
                                       used.ctypes.data_as(ctypes.c_void_p), ctypes.byref(pairs))
         dt = time.perf_counter() - t1
         assert rc == 0, env.host.svh_last_error_string()
+        ph = (ctypes.c_double * 4)()
+        env.host.svh_txset_last_phases(ph)
+        phases.append(list(ph))
         return ok, used, dt, pairs.value
 
+    phases = []
     t0 = time.perf_counter()
     built = [make(2025 + k) for k in range(sets + 1)]
     gen_s = (time.perf_counter() - t0) / (sets + 1)
     txs, cts = built[0]
     nsig = sum(len(t["sigs"]) for t in txs)
     ok_g, used_g, dt_first, pairs = run(cts, 1)
+    del phases[:]
     outs = [run(b[1], 1) for b in built[1:]]  # each distinct set once
     dts = [o[2] for o in outs]
+    ph = np.array(phases)  # the distinct sets' phases, in ms
+    phase_split = {k: float(np.median(ph[:, j])) for j, k in enumerate(
+        ("marshal_ms", "pair_enumeration_ms", "engine_prepass_ms", "checkers_ms"))}
+    phase_split["per_set"] = [[round(float(x), 3) for x in row] for row in ph]
+    phase_split["what"] = ("svh_txset_last_phases medians over the distinct sets: C structs -> mirror objects, "
+                           "SignatureBatchPrefetch::addBatch (pair enumeration), run() (one GPU batch + side "
+                           "table), the checkers on the host pool")
     dt_rep = min(run(cts, 1)[2] for _ in range(3))  # the first set again (warm per-key state): not the headline
     out = {"txs": n_tx, "decorated_signatures": nsig, "prefetched_pairs": pairs, "generate_s": gen_s,
            "distinct_sets": sets,
            "gpu_prepass_checker_s": float(np.median(dts)), "gpu_prepass_checker_max_s": float(max(dts)),
            "gpu_prepass_checker_first_call_s": dt_first, "gpu_prepass_same_set_repeat_min_s": dt_rep,
            "gpu_prepass_txs_per_s": n_tx / float(np.median(dts)),
+           "phase_split": phase_split,
            "timing": "median / max over %d distinct sets, each checked once after a first (warm-up) set; "
                      "first_call = the process's first set" % sets}
     if env.have_sodium:

@@ -34,6 +34,9 @@ def main():
         "valu_inst_per_verify": s["valu_inst_per_verify"],
         "valu_issue_util": s["valu_issue_util"],
         "l2_hit_rate": s["l2_hit_rate"],
+        # the clock the chip held over the profiled kernels (GRBM_GUI_ACTIVE /
+        # wall): bench.py's roofline.mad_issue_frac_at_profiled_clock
+        "effective_clock_ghz": s.get("effective_clock_ghz"),
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (tools/profile_run.sh), "
                   "%s/{fetch,write}_counter_collection.csv; FETCH_SIZE not doubled (per-lane 16-B gathers, "
                   "not a wide streaming read: MI355X_MICROARCH.md HBM note)" % os.path.relpath(dst, repo),
