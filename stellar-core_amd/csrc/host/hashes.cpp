@@ -2,6 +2,7 @@
 // Checked against Python hashlib in tests/test_host_mirror.py.
 #include "hashes.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -41,7 +42,6 @@ inline uint64_t load64le(const uint8_t* p) {
 Blake2b256::Blake2b256() : t_{0, 0}, fill_(0) {
   for (int i = 0; i < 8; ++i) h_[i] = kIV[i];
   h_[0] ^= 0x01010000ULL ^ 32u;  // depth 1, fanout 1, no key, digest length 32
-  std::memset(buf_, 0, sizeof buf_);
 }
 
 #if defined(__x86_64__)
@@ -78,15 +78,16 @@ __attribute__((target("avx2"))) void blake2b_compress_avx2(uint64_t h[8], const 
 #define SV_B2_M(r, i, j, k, l) \
   _mm256_setr_epi64x((long long)m[kSigma[r][i]], (long long)m[kSigma[r][j]], (long long)m[kSigma[r][k]], \
                      (long long)m[kSigma[r][l]])
+// (rows a, c, d rotate, not b: see the AVX-512 form below)
 #define SV_B2_ROUND(r)                                                                             \
   SV_B2_G(SV_B2_M(r, 0, 2, 4, 6), SV_B2_M(r, 1, 3, 5, 7))                                          \
-  b = _mm256_permute4x64_epi64(b, _MM_SHUFFLE(0, 3, 2, 1));                                        \
-  c = _mm256_permute4x64_epi64(c, _MM_SHUFFLE(1, 0, 3, 2));                                        \
-  d = _mm256_permute4x64_epi64(d, _MM_SHUFFLE(2, 1, 0, 3));                                        \
-  SV_B2_G(SV_B2_M(r, 8, 10, 12, 14), SV_B2_M(r, 9, 11, 13, 15))                                    \
-  b = _mm256_permute4x64_epi64(b, _MM_SHUFFLE(2, 1, 0, 3));                                        \
-  c = _mm256_permute4x64_epi64(c, _MM_SHUFFLE(1, 0, 3, 2));                                        \
-  d = _mm256_permute4x64_epi64(d, _MM_SHUFFLE(0, 3, 2, 1));
+  a = _mm256_permute4x64_epi64(a, _MM_SHUFFLE(2, 1, 0, 3));                                        \
+  c = _mm256_permute4x64_epi64(c, _MM_SHUFFLE(0, 3, 2, 1));                                        \
+  d = _mm256_permute4x64_epi64(d, _MM_SHUFFLE(1, 0, 3, 2));                                        \
+  SV_B2_G(SV_B2_M(r, 14, 8, 10, 12), SV_B2_M(r, 15, 9, 11, 13))                                    \
+  a = _mm256_permute4x64_epi64(a, _MM_SHUFFLE(0, 3, 2, 1));                                        \
+  c = _mm256_permute4x64_epi64(c, _MM_SHUFFLE(2, 1, 0, 3));                                        \
+  d = _mm256_permute4x64_epi64(d, _MM_SHUFFLE(1, 0, 3, 2));
   SV_B2_ROUND(0) SV_B2_ROUND(1) SV_B2_ROUND(2) SV_B2_ROUND(3) SV_B2_ROUND(4) SV_B2_ROUND(5)
   SV_B2_ROUND(6) SV_B2_ROUND(7) SV_B2_ROUND(8) SV_B2_ROUND(9) SV_B2_ROUND(10) SV_B2_ROUND(11)
 #undef SV_B2_ROUND
@@ -125,15 +126,22 @@ __attribute__((target("avx512f,avx512vl"))) void blake2b_compress_avx512(uint64_
 #define SV_B5_M(r, i, j, k, l)                                                                                  \
   _mm512_castsi512_si256(_mm512_permutex2var_epi64(                                                           \
       mlo, _mm512_setr_epi64(kSigma[r][i], kSigma[r][j], kSigma[r][k], kSigma[r][l], 0, 0, 0, 0), mhi))
+// The diagonal step rotates rows a, c and d, never b: b is the end of each
+// G's dependency chain and the next G starts with a + b, so a permute of b
+// (3 cycles) would sit on the critical path, while a, c and d were last
+// written 8, 2 and 6 operations before the end of the G and their permutes
+// overlap it.  Relative to a, the rows are then offset by (1, 2, 3) lanes, as
+// the diagonals need; lane i runs diagonal G (i + 3) % 4, so its message
+// words are sigma[8 + 2j], sigma[9 + 2j] with j = (i + 3) % 4.
 #define SV_B5_ROUND(r)                                                        \
   SV_B5_G(SV_B5_M(r, 0, 2, 4, 6), SV_B5_M(r, 1, 3, 5, 7))                     \
-  b = _mm256_permute4x64_epi64(b, _MM_SHUFFLE(0, 3, 2, 1));                   \
-  c = _mm256_permute4x64_epi64(c, _MM_SHUFFLE(1, 0, 3, 2));                   \
-  d = _mm256_permute4x64_epi64(d, _MM_SHUFFLE(2, 1, 0, 3));                   \
-  SV_B5_G(SV_B5_M(r, 8, 10, 12, 14), SV_B5_M(r, 9, 11, 13, 15))               \
-  b = _mm256_permute4x64_epi64(b, _MM_SHUFFLE(2, 1, 0, 3));                   \
-  c = _mm256_permute4x64_epi64(c, _MM_SHUFFLE(1, 0, 3, 2));                   \
-  d = _mm256_permute4x64_epi64(d, _MM_SHUFFLE(0, 3, 2, 1));
+  a = _mm256_permute4x64_epi64(a, _MM_SHUFFLE(2, 1, 0, 3));                   \
+  c = _mm256_permute4x64_epi64(c, _MM_SHUFFLE(0, 3, 2, 1));                   \
+  d = _mm256_permute4x64_epi64(d, _MM_SHUFFLE(1, 0, 3, 2));                   \
+  SV_B5_G(SV_B5_M(r, 14, 8, 10, 12), SV_B5_M(r, 15, 9, 11, 13))               \
+  a = _mm256_permute4x64_epi64(a, _MM_SHUFFLE(0, 3, 2, 1));                   \
+  c = _mm256_permute4x64_epi64(c, _MM_SHUFFLE(2, 1, 0, 3));                   \
+  d = _mm256_permute4x64_epi64(d, _MM_SHUFFLE(1, 0, 3, 2));
   SV_B5_ROUND(0) SV_B5_ROUND(1) SV_B5_ROUND(2) SV_B5_ROUND(3) SV_B5_ROUND(4) SV_B5_ROUND(5)
   SV_B5_ROUND(6) SV_B5_ROUND(7) SV_B5_ROUND(8) SV_B5_ROUND(9) SV_B5_ROUND(10) SV_B5_ROUND(11)
 #undef SV_B5_ROUND
@@ -146,19 +154,19 @@ const bool kHaveAvx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supp
                          getenv("SVH_NO_AVX512") == nullptr;
 #endif
 
-void Blake2b256::compress(bool last) {
+void Blake2b256::compress(const uint8_t* block, bool last) {
 #if defined(__x86_64__)
   if (kHaveAvx512) {
-    blake2b_compress_avx512(h_, buf_, t_[0], t_[1], last);
+    blake2b_compress_avx512(h_, block, t_[0], t_[1], last);
     return;
   }
   if (kHaveAvx2) {
-    blake2b_compress_avx2(h_, buf_, t_[0], t_[1], last);
+    blake2b_compress_avx2(h_, block, t_[0], t_[1], last);
     return;
   }
 #endif
   uint64_t m[16];
-  std::memcpy(m, buf_, sizeof m);  // (little-endian host: the words as stored)
+  std::memcpy(m, block, sizeof m);  // (little-endian host: the words as stored)
   uint64_t v0 = h_[0], v1 = h_[1], v2 = h_[2], v3 = h_[3], v4 = h_[4], v5 = h_[5], v6 = h_[6], v7 = h_[7];
   uint64_t v8 = kIV[0], v9 = kIV[1], v10 = kIV[2], v11 = kIV[3];
   uint64_t v12 = kIV[4] ^ t_[0], v13 = kIV[5] ^ t_[1], v14 = last ? ~kIV[6] : kIV[6], v15 = kIV[7];
@@ -198,29 +206,37 @@ void Blake2b256::compress(bool last) {
 }
 
 void Blake2b256::add(const uint8_t* p, size_t n) {
-  while (n > 0) {
-    if (fill_ == 128) {  // only compress when more input follows (last block is special)
-      t_[0] += 128;
-      if (t_[0] < 128) ++t_[1];
-      compress(false);
-      fill_ = 0;
-    }
-    size_t take = 128 - fill_;
-    if (take > n) take = n;
+  // a block is compressed only once more input follows it (the last block is
+  // compressed by finish() with the final flag); full blocks of the input are
+  // compressed in place, only a partial block is copied into buf_
+  if (n == 0) return;
+  if (fill_ > 0) {
+    const size_t take = std::min(128 - fill_, n);
     std::memcpy(buf_ + fill_, p, take);
     fill_ += take;
     p += take;
     n -= take;
+    if (n == 0) return;
+    bump(128);
+    compress(buf_, false);
+    fill_ = 0;
   }
+  while (n > 128) {
+    bump(128);
+    compress(p, false);
+    p += 128;
+    n -= 128;
+  }
+  std::memcpy(buf_, p, n);
+  fill_ = n;
 }
 
 Hash32 Blake2b256::finish() {
-  t_[0] += fill_;
-  if (t_[0] < fill_) ++t_[1];
+  bump(fill_);
   std::memset(buf_ + fill_, 0, 128 - fill_);
-  compress(true);
+  compress(buf_, true);
   Hash32 out;
-  for (int i = 0; i < 32; ++i) out[i] = (uint8_t)(h_[i / 8] >> (8 * (i % 8)));
+  std::memcpy(out.data(), h_, 32);  // (little-endian host: the state words as bytes)
   return out;
 }
 

@@ -22,7 +22,11 @@ class Blake2b256 {
   Hash32 finish();
 
  private:
-  void compress(bool last);
+  void compress(const uint8_t* block, bool last);
+  void bump(size_t bytes) {  // the 128-bit byte counter
+    t_[0] += bytes;
+    if (t_[0] < bytes) ++t_[1];
+  }
   uint64_t h_[8];
   uint64_t t_[2];
   uint8_t buf_[128];
