@@ -296,6 +296,13 @@ int sv_set_key_tables(int mode, size_t slots);
 #define SV_DBG_FAIL 0x4u
 #define SV_DBG_PREP_ONLY 0x8u
 #define SV_DBG_KEY_COLLIDE 0x10u /* every key gets the same per-key-table fingerprint (collision path) */
+/* throughput-path geometry: QUAD runs every throughput-path launch one signature
+ * per quad of lanes (the medium-batch kernel), NO_QUAD none (one per lane);
+ * by default launches of at most SV_QUAD_MAX signatures (env; default in
+ * DESIGN.md) that use no per-key tables take the quad geometry.  Code paths
+ * only: verdicts are unchanged. */
+#define SV_DBG_QUAD 0x20u
+#define SV_DBG_NO_QUAD 0x40u
 int sv_set_debug_flags(uint32_t flags);
 
 /* Bytes of the slot's kernel workspace / pinned staging currently allocated. */

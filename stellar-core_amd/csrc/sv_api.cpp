@@ -306,6 +306,27 @@ int resolve_path(int requested, uint64_t n) {
   if (p == SV_PATH_AUTO) p = n <= kQuickMax ? SV_PATH_LATENCY : SV_PATH_THROUGHPUT;
   return p;
 }
+
+// Throughput-path launches of at most this many signatures run one signature
+// per quad of lanes (sv_kernels.hip sv_quad_kernel): below about one wave per
+// SIMD the one-lane kernels run at a lone wave's serial latency
+// (tools/size_sweep.py).  SV_QUAD_MAX overrides (0: never).
+constexpr uint64_t kQuadMax = 65536;
+uint64_t quad_max() {
+  static const uint64_t v = env_size("SV_QUAD_MAX", kQuadMax);
+  return v;
+}
+constexpr int kGeomQuad = 3;  // sv_launch_verify's path code of the quad geometry
+// The kernel geometry of a launch of n on resolved path rp.  (A quad launch
+// decodes every key itself: the per-key tables only serve the one-lane
+// kernels of larger launches.)
+int launch_geometry(int rp, uint64_t n) {
+  if (rp != SV_PATH_THROUGHPUT) return rp;
+  const uint32_t d = g_dbg.load();
+  if (d & SV_DBG_NO_QUAD) return rp;
+  if (d & SV_DBG_QUAD) return kGeomQuad;
+  return n <= quad_max() ? kGeomQuad : rp;
+}
 int path_from_flags(uint32_t flags) {
   if (flags & SV_FLAG_PATH_LATENCY) return SV_PATH_LATENCY;
   if (flags & SV_FLAG_PATH_THROUGHPUT) return SV_PATH_THROUGHPUT;
@@ -567,9 +588,10 @@ int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig
   const bool share = rp != SV_PATH_LATENCY && share_now(D);
   const unsigned grid = grid_for(D, n, share);
   int rc;
-  if ((rc = ensure_ws(D, sv_verify_ws_bytes(rp, grid, n)))) return rc;
   sv_ktparams ktp{};
-  const bool kt_on = tables && rp != SV_PATH_LATENCY && kt_prepare(D, n, &ktp);
+  const int geom = launch_geometry(rp, n);
+  const bool kt_on = tables && geom == SV_PATH_THROUGHPUT && kt_prepare(D, n, &ktp);
+  if ((rc = ensure_ws(D, sv_verify_ws_bytes(geom, grid, n)))) return rc;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool timing = g_timing.load() != 0;
   if (timing) {
@@ -577,7 +599,7 @@ int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig
     SV_HIP(hipEventCreate(&e1));
     SV_HIP(hipEventRecord(e0, D.stream));
   }
-  SV_HIP(sv_launch_verify(mode, rp, grid, pk, sig, msg, off, len, fixed_len, n, verdict, bitmap, D.ws.p, D.btab,
+  SV_HIP(sv_launch_verify(mode, geom, grid, pk, sig, msg, off, len, fixed_len, n, verdict, bitmap, D.ws.p, D.btab,
                           g_dbg.load() & kKernelDbgMask, share ? 1 : 0, kt_on ? &ktp : nullptr, D.stream));
   if (share) D.shared_launches.fetch_add(1, std::memory_order_relaxed);
   if (kt_on) {
@@ -900,8 +922,12 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
               trace_abs_us());
   };
   // the largest launch first, so the workspace never grows under a running kernel
-  if (verdict && (rc = ensure_ws(D, sv_verify_ws_bytes(resolve_path(path, chunk), grid_for(D, chunk), chunk))))
-    return rc;
+  if (verdict) {
+    const int rp = resolve_path(path, chunk);
+    const size_t wb = std::max(sv_verify_ws_bytes(rp, grid_for(D, chunk), chunk),
+                               sv_verify_ws_bytes(launch_geometry(rp, chunk), grid_for(D, chunk), chunk));
+    if ((rc = ensure_ws(D, wb))) return rc;
+  }
   trace_at("workspace");
   const size_t out_per = (verdict ? 1 : 0) + (keys ? 32 : 0);
   // one chunk (latency-bound batches): everything on the kernel stream, no
@@ -1981,8 +2007,10 @@ int sv_set_kernel_path(int path) {
 
 int sv_set_debug_flags(uint32_t flags) {
   LifeGuard life_;
-  if (flags & ~(SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_FAIL | SV_DBG_PREP_ONLY | SV_DBG_KEY_COLLIDE))
+  if (flags & ~(SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_FAIL | SV_DBG_PREP_ONLY | SV_DBG_KEY_COLLIDE |
+                SV_DBG_QUAD | SV_DBG_NO_QUAD))
     return SV_ERR_INVALID_ARG;
+  if ((flags & SV_DBG_QUAD) && (flags & SV_DBG_NO_QUAD)) return SV_ERR_INVALID_ARG;
   // the knobs that change what a call returns (FAIL: every call errs;
   // PREP_ONLY: no verdicts) only exist for processes that opt in
   if ((flags & (SV_DBG_FAIL | SV_DBG_PREP_ONLY)) && !test_knobs_enabled())

@@ -29,6 +29,9 @@
 // from the record and one base address per staged entry it fits without
 // spills in the loop; measured 1-1.5 % faster than 2 waves
 // (profiles/r02/ab_main_waves.txt)
+#ifndef SV_QUAD_WAVES
+#define SV_QUAD_WAVES 3  // sv_quad_kernel (medium batches), waves per SIMD
+#endif
 #ifndef SV_MAIN_WAVES
 #define SV_MAIN_WAVES 3
 #endif
@@ -692,6 +695,164 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
   }
 }
 
+// ------------------------------------------- medium batches: one signature per quad
+// Between the latency path and full throughput, a batch of n signatures gives
+// the one-lane kernels n / 64 waves: under one per SIMD up to 64k signatures,
+// each at a lone wave's serial latency (the one-lane prep + main stream of a
+// wave is ~0.3M instructions).  Here a QUAD of lanes evaluates one
+// signature's whole half-size equation (*) (lattice.h), 16 signatures per
+// wave and 4x the waves, each with a ~3x shorter instruction stream:
+//   * all four lanes load, hash, check and run the Euclid reduction (one
+//     instruction stream whatever the number of lanes: free in latency);
+//   * lanes 0 / 2 decode -A while lanes 1 / 3 decode -R (the same code);
+//   * the quad builds both 9-entry tables with quad-split additions (qd_add)
+//     into the chunk workspace, each lane storing (and later reading) only
+//     its own operands;
+//   * the throughput path's joint chain (4 doublings, the -A and -R entries,
+//     on base windows the e B and e 2^128 B entries) runs in own form
+//     (quad.h), each window's entries loaded before its doublings.
+// Same field operations, bounds and decisions as the one-lane path, so the
+// verdicts are identical (every fixture class is GPU-tested on it).
+#define SV_QSIGS 16
+// A table entry holds each lane's operands in a region of its own, so every
+// lane only ever reads back what it wrote itself (no cross-lane memory
+// ordering inside the wave): lane 0 (Y+X, Y-X), lane 1 (Y-X, Y+X) -- the pair
+// read straight or swapped by a digit's sign, qo_load_cached's roles -- lane 2
+// Z, lane 3 2dT.  60 dwords per entry, 2 x 9 entries per signature.
+#define SV_QENT 60
+#define SV_QSLOT_QUADS (2 * SV_ATAB_ENTRIES * SV_QENT / 4)
+__device__ __forceinline__ uint32_t qd_swap1(uint32_t v) {  // lane r ^ 1 of the quad
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t sv_qoff(uint32_t role) { return role < 2 ? 20u * role : 40u + 10u * (role - 2); }
+__device__ __forceinline__ void sv_qst10(uint32_t* d, const fe& x) {
+  uint2* p = (uint2*)d;
+  SV_UNROLL for (int k = 0; k < 5; ++k) p[k] = uint2{x.v[2 * k], x.v[2 * k + 1]};
+}
+// this lane's operands of cached entry c into table entry `ent`
+__device__ __forceinline__ void sv_qstore(uint32_t* ent, const ge_cached& c, const qd_role& q, uint32_t role) {
+  fe x, y;
+  fe_pick4(x, q, c.YpX, c.YmX, c.Z, c.T2d);  // the operand read straight ...
+  fe_pick4(y, q, c.YmX, c.YpX, c.Z, c.T2d);  // ... and swapped (roles 0, 1)
+  uint32_t* d = ent + sv_qoff(role);
+  sv_qst10(d, x);
+  if (role < 2) sv_qst10(d + 10, y);
+}
+// this lane's operand of entry `ent` with a digit's sign (qo_load_cached's)
+__device__ __forceinline__ void sv_qload(fe& o, const uint32_t* ent, uint32_t role, bool neg) {
+  const uint2* p = (const uint2*)(ent + sv_qoff(role) + (role < 2 && neg ? 10u : 0u));
+  SV_UNROLL for (int k = 0; k < 5; ++k) {
+    const uint2 v = p[k];
+    o.v[2 * k] = v.x;
+    o.v[2 * k + 1] = v.y;
+  }
+}
+// {0..8}(P) in cached form, P affine (ge_frombytes) and whole on every lane
+__device__ __forceinline__ void sv_qbuild(uint32_t* tab, const ge_p3& P, const qd_role& q, uint32_t role) {
+  ge_cached c1, ce;
+  ge_p3_to_cached(c1, P);
+  ge_cached_identity(ce);
+  sv_qstore(tab, ce, q, role);
+  sv_qstore(tab + SV_QENT, c1, q, role);
+  fe mine;
+  fe_pick4(mine, q, c1.T2d, c1.Z, c1.YpX, c1.YmX);  // (qd_add's operand order)
+  ge_p3 P3 = P;
+  SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
+    qd_add(P3, mine, q, false, true);
+    ge_p3_to_cached(ce, P3);
+    sv_qstore(tab + e * SV_QENT, ce, q, role);
+  }
+}
+template <int MODE, bool MSG>
+__global__ __launch_bounds__(64, SV_QUAD_WAVES) void sv_quad_kernel(sv_kparams p) {
+  __shared__ sv_u4 s_msg[MSG ? SV_QSIGS * (SV_MSG_CAP / 16) : 1];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t role = lane & 3u, sq = lane >> 2;
+  const qd_role q{role == 1, role == 2, role == 3};
+  const uint64_t i = (uint64_t)blockIdx.x * SV_QSIGS + sq;
+  const bool active = i < p.n;
+  const uint64_t ii = active ? i : p.n - 1;  // idle tail quads redo the last item (own slots)
+  uint32_t A[8], S[8], hram[16], R[8];
+  if (MSG) sv_load_and_hash_lds<MODE, 4>(p, ii, role, s_msg + sq * (SV_MSG_CAP / 16), A, S, hram);
+  else sv_load_and_hash<MODE>(p, ii, A, S, hram);
+  sv_unpack2(R, p.sig + 4 * ii);
+  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
+            sv_point_canonical(R);
+  sv_lat lat;
+  {
+    uint32_t h[8];
+    sc_reduce512(h, hram);
+    sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
+  }
+  const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
+  sv_lat_digits D;
+  sv_lat_prepare(D, lat, S, W);
+  // decode: lanes 0, 2 -A, lanes 1, 3 -R; then both tables on the whole quad
+  uint32_t* tabA = (uint32_t*)(p.ws + i * SV_QSLOT_QUADS);
+  uint32_t* tabR = tabA + SV_ATAB_ENTRIES * SV_QENT;
+  {
+    uint32_t E[8];
+    SV_UNROLL for (int k = 0; k < 8; ++k) E[k] = (role & 1u) ? R[k] : A[k];
+    ge_p3 Pt;
+    const uint32_t dk = ge_frombytes(Pt, E, true) ? 1u : 0u;
+    ok = ok && (dk & qd_swap1(dk)) != 0;
+    ge_p3 Pq;
+    fe_from<0>(Pq.X, Pt.X);
+    fe_from<0>(Pq.Y, Pt.Y);
+    fe_from<0>(Pq.Z, Pt.Z);
+    fe_from<0>(Pq.T, Pt.T);
+    sv_qbuild(tabA, Pq, q, role);
+    fe_from<1>(Pq.X, Pt.X);
+    fe_from<1>(Pq.Y, Pt.Y);
+    fe_from<1>(Pq.Z, Pt.Z);
+    fe_from<1>(Pq.T, Pt.T);
+    sv_qbuild(tabR, Pq, q, role);
+  }
+  const sv_u4* btab0 = p.btab;
+  const sv_u4* btab1 = p.btab + SV_LBTAB_ENTRIES * SV_BTAB_QUADS;
+  fe h;
+  qo_identity(h, q);
+  SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
+    int32_t dA = sc_pop_top(D.dA, 4), dR = sc_pop_top(D.dR, 4);
+    if (w == W - 1) {
+      if (D.top8A) dA = 8;
+      if (D.top8R) dR = 8;
+    }
+    if (D.rneg) dR = -dR;
+    int32_t dB0, dB1;
+    const bool bwin = sv_lat_bdigits(D, w, dB0, dB1);
+    // the window's entries, loaded before its doublings
+    fe ma, mr, m0;
+    sv_qload(ma, tabA + (dA < 0 ? -dA : dA) * SV_QENT, role, dA < 0);
+    sv_qload(mr, tabR + (dR < 0 ? -dR : dR) * SV_QENT, role, dR < 0);
+    if (bwin) qo_load_affine(m0, btab0 + (dB0 < 0 ? -dB0 : dB0) * SV_BTAB_QUADS, role, dB0 < 0);
+    if (w != W - 1) {
+      SV_NOUNROLL for (int k = 0; k < 4; ++k) qo_dbl(h, q);
+    }
+    qo_add(h, ma, q, dA < 0);
+    if (bwin) qo_load_affine(ma, btab1 + (dB1 < 0 ? -dB1 : dB1) * SV_BTAB_QUADS, role, dB1 < 0);
+    qo_add(h, mr, q, dR < 0);
+    if (bwin) {
+      qo_add(h, m0, q, dB0 < 0);
+      qo_add(h, ma, q, dB1 < 0);
+    }
+  }
+  ge_p3 P;
+  qo_expand(P, h);
+  ok = ok && sv_is_identity(P);
+  const bool owner = role == 0;
+  if (active && owner) p.verdict[i] = ok ? 1 : 0;
+  const uint64_t bal = __ballot(ok && active && owner);
+  if (p.bitmap != nullptr && lane == 0) {
+    uint32_t m16 = 0;
+    SV_UNROLL for (int k = 0; k < SV_QSIGS; ++k) m16 |= (uint32_t)((bal >> (4 * k)) & 1u) << k;
+    ((uint16_t*)p.bitmap)[blockIdx.x] = (uint16_t)m16;
+    // the last workgroup clears the rest of the final 64-bit word (bits past n read as 0)
+    if (blockIdx.x == gridDim.x - 1)
+      for (uint32_t b = blockIdx.x + 1; b % 4 != 0; ++b) ((uint16_t*)p.bitmap)[b] = 0;
+  }
+}
+
 __global__ __launch_bounds__(192) void sv_btab_init_kernel(uint32_t* btab) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   // table 0: e B (also the signer's table: it reads entries <= 2^(SV_B_BITS-1));
@@ -823,6 +984,23 @@ static size_t sv_prep_share_lds(void) {
   b = (b + 255) & ~(size_t)255;
   return b > 65536 ? 65536 : b;
 }
+// Shared mode for the quad kernel (one-wave workgroups, SV_QUAD_WAVES per
+// SIMD): dynamic LDS such that at most 4 (SV_QUAD_WAVES - 1) fit per CU and
+// 32 KiB of LDS stay free, which leaves a latency workgroup room on each CU.
+static size_t sv_quad_share_lds(void) {
+  int v = g_lds_cu.load(std::memory_order_relaxed);
+  if (v == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess || v < 1)
+      v = 160 * 1024;
+    g_lds_cu.store(v, std::memory_order_relaxed);
+  }
+  const int blocks = 4 * (SV_QUAD_WAVES > 1 ? SV_QUAD_WAVES - 1 : 1);
+  size_t b = ((size_t)v - 32 * 1024) / (size_t)blocks;
+  b &= ~(size_t)255;
+  return b > 65536 ? 65536 : b;
+}
 // SIMDs of the current device (4 per CU)
 static std::atomic<int> g_cus[64];
 static uint64_t sv_device_simds(void) {
@@ -890,6 +1068,7 @@ size_t sv_ws_bytes(unsigned grid, uint64_t cap) {
 size_t sv_verify_ws_bytes(int path, unsigned grid, uint64_t n) {
   if (path == 2) return 0;
   (void)grid;
+  if (path == 3) return (size_t)((n + SV_QSIGS - 1) / SV_QSIGS * SV_QSIGS) * SV_QSLOT_QUADS * sizeof(sv_u4);
   return sv_ws_bytes(0, sv_ws_cap(n));
 }
 #define SV_BTAB_TOTAL (2 * SV_LBTAB_ENTRIES)
@@ -951,7 +1130,17 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
 #undef SV_OCTET_LAUNCH
     return hipGetLastError();
   }
-  (void)path;
+  if (path == 3) {  // the throughput path's medium-batch geometry (sv_quad_kernel)
+    const unsigned qg = (unsigned)((n + SV_QSIGS - 1) / SV_QSIGS);
+    const bool msg = mode != 0;
+    const size_t qlds = share ? sv_quad_share_lds() : 0;
+#define SV_QUAD_LAUNCH(M, G) hipLaunchKernelGGL((sv_quad_kernel<M, G>), dim3(qg), dim3(64), qlds, s, p)
+    if (mode == 0) SV_QUAD_LAUNCH(0, false);
+    else if (mode == 1 && msg) SV_QUAD_LAUNCH(1, true);
+    else SV_QUAD_LAUNCH(2, true);
+#undef SV_QUAD_LAUNCH
+    return hipGetLastError();
+  }
   const uint64_t cap = sv_ws_cap(n);
   const uint64_t chunk = sv_plan_chunk(n, share);
   const size_t plds = share ? sv_prep_share_lds() : 0;

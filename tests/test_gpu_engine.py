@@ -26,12 +26,18 @@ def dev(sv):
     return torch.device("cuda", 0)
 
 
-@pytest.fixture(params=["throughput", "latency"])
+@pytest.fixture(params=["throughput", "quad", "latency"])
 def kpath(sv, request):
-    code = {"throughput": sv.PATH_THROUGHPUT, "latency": sv.PATH_LATENCY}[request.param]
+    """(throughput: the one-lane kernels, quad: one signature per quad; both on
+    SV_PATH_THROUGHPUT.  geom holds the geometry's debug flag, for tests that
+    set flags of their own.)"""
+    code = {"throughput": sv.PATH_THROUGHPUT, "quad": sv.PATH_THROUGHPUT, "latency": sv.PATH_LATENCY}[request.param]
+    geom = {"throughput": sv.DBG_NO_QUAD, "quad": sv.DBG_QUAD}.get(request.param, 0)
     prev = sv.set_kernel_path(code)
-    yield request.param
+    prev_dbg = sv.set_debug_flags(geom)
+    yield geom
     sv.set_kernel_path(prev)
+    sv.set_debug_flags(prev_dbg)
 
 
 def gpu_sign(sv, dev, seeds, msgs):
@@ -62,7 +68,7 @@ def test_forced_trivial_pair_and_max_windows(sv, dev, golden, kpath, flags):
     branches)."""
     f = {"trivial_pair": sv.DBG_TRIVIAL_PAIR, "max_windows": sv.DBG_MAX_WINDOWS,
          "both": sv.DBG_TRIVIAL_PAIR | sv.DBG_MAX_WINDOWS}[flags]
-    prev = sv.set_debug_flags(f)
+    prev = sv.set_debug_flags(f | kpath)
     try:
         for name in ("intree", "adversarial", "lattice_edge", "msglen"):
             d = golden[name]

@@ -30,7 +30,10 @@ def dev(sv):
 
 @pytest.fixture
 def tables(sv, dev):
+    # (the per-key tables serve the one-lane kernels: medium launches would
+    # otherwise take the quad geometry, which decodes every key itself)
     prev = sv.set_key_tables(1)
+    sv.set_debug_flags(sv.DBG_NO_QUAD)
     yield sv
     sv.set_key_tables(prev)
     sv.set_debug_flags(0)
@@ -98,7 +101,7 @@ def test_adversarial_keys_cached_as_rejecting(tables, golden):
 def test_fingerprint_collisions_fall_back(tables, dev):
     sv = tables
     pk, sig, msgs, want = repeated_set(sv, dev, 512, 64, seed=2)
-    sv.set_debug_flags(sv.DBG_KEY_COLLIDE)
+    sv.set_debug_flags(sv.DBG_KEY_COLLIDE | sv.DBG_NO_QUAD)
     for _ in range(2):
         assert np.array_equal(verify_dev(sv, dev, pk, sig, msgs), want)
 
@@ -118,6 +121,7 @@ def test_small_tables_clear_and_refill(tables, dev):
 
 def test_auto_mode_uses_tables_for_repeated_host_keys(sv, dev):
     prev = sv.set_key_tables(2)
+    prev_dbg = sv.set_debug_flags(sv.DBG_NO_QUAD)
     try:
         pk, sig, msgs, want = repeated_set(sv, dev, 512, 64, seed=4)
         P, S, M = pk.cpu().numpy(), sig.cpu().numpy(), msgs.cpu().numpy()
@@ -132,3 +136,4 @@ def test_auto_mode_uses_tables_for_repeated_host_keys(sv, dev):
         assert sv.key_cache_stats(0)["table_launches"] == t1
     finally:
         sv.set_key_tables(prev)
+        sv.set_debug_flags(prev_dbg)

@@ -33,9 +33,14 @@ def gpu(sv):
     return 0
 
 
-@pytest.fixture(params=["auto", "throughput", "latency"])
-def path(request):
-    return request.param
+@pytest.fixture(params=["auto", "throughput", "quad", "latency"])
+def path(request, sv):
+    """The per-call path; "throughput" forces the one-lane kernels and "quad"
+    one signature per quad of lanes (the throughput path's two geometries)."""
+    geom = {"throughput": sv.DBG_NO_QUAD, "quad": sv.DBG_QUAD}.get(request.param, 0)
+    prev = sv.set_debug_flags(geom)
+    yield "throughput" if request.param == "quad" else request.param
+    sv.set_debug_flags(prev)
 
 
 def _rows(d, rows):

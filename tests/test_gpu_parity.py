@@ -34,15 +34,21 @@ def dev(sv):
     return torch.device("cuda", 0)
 
 
-@pytest.fixture(params=["auto", "throughput", "latency"])
+@pytest.fixture(params=["auto", "throughput", "quad", "latency"])
 def kpath(sv, request):
-    """Runs the test on each kernel path (include/stellar_sigverify.h SV_PATH_*):
-    the one-lane prep + main kernels and the quad-per-signature latency kernel
-    must give identical verdicts."""
-    code = {"auto": sv.PATH_AUTO, "throughput": sv.PATH_THROUGHPUT, "latency": sv.PATH_LATENCY}[request.param]
+    """Runs the test on each kernel path (include/stellar_sigverify.h SV_PATH_*)
+    and throughput-path geometry: the one-lane prep + main kernels
+    (throughput, SV_DBG_NO_QUAD), one signature per quad (quad, SV_DBG_QUAD:
+    the medium-batch kernel) and the octet latency kernel must give identical
+    verdicts."""
+    code = {"auto": sv.PATH_AUTO, "throughput": sv.PATH_THROUGHPUT, "quad": sv.PATH_THROUGHPUT,
+            "latency": sv.PATH_LATENCY}[request.param]
+    geom = {"throughput": sv.DBG_NO_QUAD, "quad": sv.DBG_QUAD}.get(request.param, 0)
     prev = sv.set_kernel_path(code)
+    prev_dbg = sv.set_debug_flags(geom)
     yield request.param
     sv.set_kernel_path(prev)
+    sv.set_debug_flags(prev_dbg)
 
 
 def _seed_msg(lo, hi):
@@ -81,6 +87,8 @@ def test_per_call_path_flags(sv, dev, golden):
     for path in ("throughput", "latency"):
         out = sv.verify_batch(d["pk"], d["sig"], d["msg"], d["msg_off"], d["msg_len"], device=0, path=path)
         assert (out == d["verdict"]).all(), path
+    with pytest.raises(sv.SigVerifyError):  # both geometries forced at once
+        sv.set_debug_flags(sv.DBG_QUAD | sv.DBG_NO_QUAD)
     with pytest.raises(sv.SigVerifyError):
         sv.verify_batch(d["pk"][:1], d["sig"][:1], d["msg"], d["msg_off"][:1], d["msg_len"][:1], device=0, path=3)
 
