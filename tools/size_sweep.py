@@ -4,9 +4,11 @@ sizes, kernel-only (HIP events around the launches, device-resident input) and
 per call (host API from pageable arrays), to set the auto crossover
 (kQuickMax, csrc/sv_api.cpp) from measurements on the current kernels.
 
-  throughput  one lane per signature (prep + persistent main kernel)
+  throughput  one lane per signature (prep + persistent main kernel; SV_DBG_NO_QUAD)
+  quad        one signature per quad of lanes (sv_quad_kernel; SV_DBG_QUAD)
   latency     the octet kernel, key cache off (the cold-key latency path: what a
               tx set's mostly distinct signers get)
+  auto        the engine's own choice
 
 32-byte messages, keys and signatures made on the GPU, 1/16 of the rows
 corrupted; every call's verdicts are checked.  Prints one JSON line.
@@ -47,8 +49,14 @@ def main():
     out_d = torch.zeros(n_max, dtype=torch.uint8, device=dev)
     sv.set_key_cache(0)
     res = {"iters": iters, "sizes": list(sizes), "paths": {}}
-    for name, code in (("throughput", sv.PATH_THROUGHPUT), ("latency", sv.PATH_LATENCY)):
+    paths = (("throughput", sv.PATH_THROUGHPUT, sv.DBG_NO_QUAD), ("quad", sv.PATH_THROUGHPUT, sv.DBG_QUAD),
+             ("latency", sv.PATH_LATENCY, 0), ("auto", sv.PATH_AUTO, 0))
+    only = os.environ.get("SWEEP_PATHS")
+    for name, code, dbg in paths:
+        if only and name not in only.split(","):
+            continue
         prev = sv.set_kernel_path(code)
+        prev_dbg = sv.set_debug_flags(dbg)
         rows = {}
         for n in sizes:
             if name == "latency" and n > 131072:
@@ -87,6 +95,7 @@ def main():
             print(name, n, json.dumps(rows[str(n)]), file=sys.stderr, flush=True)
         res["paths"][name] = rows
         sv.set_kernel_path(prev)
+        sv.set_debug_flags(prev_dbg)
     sv.set_key_cache(1024)
     print(json.dumps(res), flush=True)
 
