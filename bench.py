@@ -429,7 +429,7 @@ class ScpResult(ctypes.Structure):
                                                   "max_batch")]
                 + [("mean_batch", ctypes.c_double)]
                 + [(k, ctypes.c_uint64) for k in ("gpu_batches", "gpu_signatures", "cpu_signatures", "fallbacks")]
-                + [("wall_s", ctypes.c_double)])
+                + [(k, ctypes.c_double) for k in ("wall_s", "ready_p50_us", "ready_p99_us")])
 
 
 def scp_envelope_set(sodium, n, seed, adversarial=0.1, validators=100):

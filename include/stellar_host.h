@@ -231,6 +231,7 @@ typedef struct svh_scp_result {
   double mean_batch;
   uint64_t gpu_batches, gpu_signatures, cpu_signatures, fallbacks; /* engine counts over the run */
   double wall_s; /* first submission -> last main-thread verifySig */
+  double ready_p50_us, ready_p99_us; /* submit -> the item's batch verified and cached (before its continuations) */
 } svh_scp_result;
 int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                 const uint32_t* msg_len, size_t n, const svh_scp_params* params, uint8_t* verdict,

@@ -448,6 +448,7 @@ int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
     o.policy = prm->policy == 1 ? VerifyMicroBatcher::FlushPolicy::Deadline : VerifyMicroBatcher::FlushPolicy::WhenIdle;
     o.idleInFlight = std::max(1u, prm->idle_in_flight);
     o.linger = std::chrono::microseconds(prm->linger_us);
+    o.recordLatency = true;  // (submit -> the batch's verdicts are in the cache, before its continuations run)
     std::vector<Clk::time_point> tSub(n), tVer(n), tMain(n);
     std::vector<uint8_t> cbVerdict(n, 2);
     // the main thread's queue (Peer::recvMessage posted by the continuation)
@@ -521,6 +522,12 @@ int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
       mainThr.join();
       mb.drain();
       st = mb.stats();
+      std::vector<double> ready = mb.latencies();
+      std::sort(ready.begin(), ready.end());
+      if (!ready.empty()) {
+        res->ready_p50_us = ready[ready.size() / 2];
+        res->ready_p99_us = ready[std::min(ready.size() - 1, (size_t)(0.99 * (double)ready.size()))];
+      }
     }
     auto eng = PubKeyUtils::flushEngineCounts();
     std::vector<double> lv(n), lm(n);

@@ -7,6 +7,10 @@
 
 struct sv_u4;  // (verify_core.h: 16-byte quad)
 
+// (sv_kparams::dbg bit set by the host, never a user flag) the launch serves
+// the latency lane: the kernel raises its waves' priority (s_setprio 3)
+#define SV_KP_LAT 0x80000000u
+
 #define SV_KT_TQUADS 90  // table_A: SV_ATAB_ENTRIES x SV_LTAB_QUADS (checked in sv_kernels.hip)
 #define SV_KT_QUADS (SV_KT_TQUADS + 3)                   // + pk (2 quads) + status
 #define SV_KT_NONE 0xffffffffu

@@ -199,6 +199,7 @@ struct LatLane {
   HostBuf z_out;   // mapped: the kernels write verdicts in place
   HostBuf z_keys;  // mapped: the hash kernel writes cache keys in place (keyed batches)
   DevBuf d_in, d_out, d_keys, d_build;
+  DevBuf ws;  // the quad kernel's tables (cold batches above kOctetMax)
   void* ctab = nullptr;  // tables of B (built at lane init)
   DevBuf ktab, kstat;    // tables of -A per cached key, status per slot
   size_t cap = 0;        // key-cache capacity the index / tables are sized for
@@ -311,7 +312,12 @@ int resolve_path(int requested, uint64_t n) {
 // per quad of lanes (sv_kernels.hip sv_quad_kernel): below about one wave per
 // SIMD the one-lane kernels run at a lone wave's serial latency
 // (tools/size_sweep.py).  SV_QUAD_MAX overrides (0: never).
-constexpr uint64_t kQuadMax = 65536;
+constexpr uint64_t kQuadMax = 32768;
+// Cold latency-lane batches above this size run the quad kernel (on the
+// lane, at wave priority 3) instead of the octet kernel: one signature per 4
+// lanes instead of 16 overtakes the octet's shorter chains from ~6k
+// signatures (tools/size_sweep.py, profiles/r05/size_sweep/).
+constexpr uint64_t kOctetMax = 6144;
 uint64_t quad_max() {
   static const uint64_t v = env_size("SV_QUAD_MAX", kQuadMax);
   return v;
@@ -1139,6 +1145,7 @@ void release_lat(LatLane& L) {
   L.z_out.release();
   L.z_keys.release();
   L.d_in.release(); L.d_out.release(); L.d_keys.release(); L.d_build.release();
+  L.ws.release();
   L.ktab.release(); L.kstat.release();
   if (L.ctab) (void)hipFree(L.ctab);
   L.ctab = nullptr;
@@ -1450,7 +1457,11 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
       SV_HIP(sv_launch_comb(mode, bulk_busy ? 1 : sv_comb_spw(n, D.cus), d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
                             d_verdict, (const uint32_t*)(d + o_ks), (const uint32_t*)L.ktab.p,
                             (const uint32_t*)L.kstat.p, (const uint32_t*)L.ctab, L.stream));
-    else
+    else if (n > kOctetMax && !(g_dbg.load() & SV_DBG_NO_QUAD)) {
+      if ((rc = L.ws.ensure(sv_verify_ws_bytes(kGeomQuad, 0, n)))) return rc;
+      SV_HIP(sv_launch_verify(mode, kGeomQuad, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n, d_verdict,
+                              nullptr, L.ws.p, D.btab, dbg | SV_KP_LAT, 0, nullptr, L.stream));
+    } else
       SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
                               d_verdict, nullptr, nullptr, D.btab, dbg, 0, nullptr, L.stream));
     if ((rc = lat_timing_end(L, e0, n))) return rc;
@@ -1971,9 +1982,13 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
     SV_HIP(hipEventRecord(L.ev_lat, user));
     SV_HIP(hipStreamWaitEvent(L.stream, L.ev_lat, 0));
     hipEvent_t e0;
+    const uint32_t dbg = g_dbg.load() & kKernelDbgMask;
+    const bool quad = n > kOctetMax && !(g_dbg.load() & SV_DBG_NO_QUAD);
+    if (quad && (rc = L.ws.ensure(sv_verify_ws_bytes(kGeomQuad, 0, n)))) return rc;
     if ((rc = lat_timing_begin(L, &e0))) return rc;
-    SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d_pk, d_sig, d_msg, d_msg_off, d_msg_len, fixed_msg_len, n,
-                            d_verdict, d_bitmap, nullptr, D.btab, g_dbg.load() & kKernelDbgMask, 0, nullptr, L.stream));
+    SV_HIP(sv_launch_verify(mode, quad ? kGeomQuad : SV_PATH_LATENCY, 1, d_pk, d_sig, d_msg, d_msg_off, d_msg_len,
+                            fixed_msg_len, n, d_verdict, d_bitmap, quad ? L.ws.p : nullptr, D.btab,
+                            quad ? (dbg | SV_KP_LAT) : dbg, 0, nullptr, L.stream));
     if ((rc = lat_timing_end(L, e0, n))) return rc;
     SV_HIP(hipEventRecord(L.done, L.stream));
     SV_HIP(hipStreamWaitEvent(user, L.done, 0));

@@ -766,6 +766,7 @@ __device__ __forceinline__ void sv_qbuild(uint32_t* tab, const ge_p3& P, const q
 template <int MODE, bool MSG>
 __global__ __launch_bounds__(64, SV_QUAD_WAVES) void sv_quad_kernel(sv_kparams p) {
   __shared__ sv_u4 s_msg[MSG ? SV_QSIGS * (SV_MSG_CAP / 16) : 1];
+  if (p.dbg & SV_KP_LAT) __builtin_amdgcn_s_setprio(3);  // (on the latency lane: as the octet / comb kernels)
   const uint32_t lane = threadIdx.x;
   const uint32_t role = lane & 3u, sq = lane >> 2;
   const qd_role q{role == 1, role == 2, role == 3};

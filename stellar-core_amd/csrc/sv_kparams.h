@@ -2,6 +2,7 @@
 // kernel translation units (sv_kernels.hip, sv_comb.hip).
 #pragma once
 
+#include "keytab.h"
 #include "verify_core.h"
 
 struct sv_kparams {
@@ -16,7 +17,7 @@ struct sv_kparams {
   uint64_t* bitmap;       // optional, ceil(n/64) words
   sv_u4* ws;              // workspace: grid threads x SV_SLOT_QUADS (lane-major)
   const sv_u4* btab;      // SV_BTAB_ENTRIES x 9 quads (global copy)
-  uint32_t dbg;           // SV_DBG_* test knobs (sv_set_debug_flags), 0 in production
+  uint32_t dbg;           // SV_DBG_* test knobs (sv_set_debug_flags), 0 in production; + SV_KP_LAT (keytab.h)
 };
 
 __device__ __forceinline__ void sv_unpack2(uint32_t w[8], const sv_u4* p) {

@@ -1,0 +1,11 @@
+# Round 5: GPU suite on the quad geometry + lane cold-quad routing; the
+# integrated config-4 probe (with host / lane traces); the size sweep's auto
+# column over the new crossovers.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/${1:-r5b}; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1 || exit $?
+timeout -k 10 300 python -u tools/scp_probe.py 12000 "1000:5000:0:1:2:4,1000:5000:100:1:2:4,1000:5000:0:2:2:4,1000:5000:0:1:1:1,250:1250:0:1:2:4" > $OUT/scp_probe.jsonl 2> $OUT/scp_probe.err || exit $?
+SV_HOST_TRACE=1 SV_LAT_TRACE=1 timeout -k 10 300 python -u tools/scp_probe.py 6000 "1000:5000:0:1:2:4" > $OUT/scp_trace.jsonl 2> $OUT/scp_trace.err || exit $?
+SWEEP_PATHS=auto,latency timeout -k 10 400 python -u tools/size_sweep.py 15 "4096,6144,8192,10240,12288,16384,29217,32768,40960" > $OUT/size_sweep.json 2> $OUT/size_sweep.err || exit $?
