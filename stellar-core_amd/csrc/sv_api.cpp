@@ -194,6 +194,7 @@ struct LatLane {
   bool ready = false;
   hipStream_t stream = nullptr;  // verify work (highest priority)
   hipStream_t build = nullptr;   // key-table builds (lowest priority)
+  hipStream_t hstream = nullptr; // a keyed batch's cache keys, beside the verify kernel (highest priority)
   hipEvent_t ev_lat = nullptr, done = nullptr, keys_down = nullptr;
   HostBuf h_in, h_out, h_build;
   HostBuf z_out;   // mapped: the kernels write verdicts in place
@@ -1134,6 +1135,7 @@ void release_lat(LatLane& L) {
   if (!L.ready) return;
   (void)hipStreamSynchronize(L.stream);
   (void)hipStreamSynchronize(L.build);
+  if (L.hstream) (void)hipStreamSynchronize(L.hstream);
   lat_drop_builds(L);
   for (auto& pr : L.pending) {
     (void)hipEventDestroy(pr.first);
@@ -1155,7 +1157,8 @@ void release_lat(LatLane& L) {
   L.ev_lat = L.done = L.keys_down = nullptr;
   if (L.stream) (void)hipStreamDestroy(L.stream);
   if (L.build) (void)hipStreamDestroy(L.build);
-  L.stream = L.build = nullptr;
+  if (L.hstream) (void)hipStreamDestroy(L.hstream);
+  L.stream = L.build = L.hstream = nullptr;
   L.index.reset(0);
   L.cap = 0;
   L.ready = false;
@@ -1180,6 +1183,7 @@ int lat_ready(Device& D) {
   L.h_in.mapped = true;  // (the kernels read it in place: lat_in_place)
   L.ready = true;  // (release_lat cleans up whatever exists from here on)
   hipError_t e = hipStreamCreateWithPriority(&L.build, hipStreamNonBlocking, least);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&L.hstream, hipStreamNonBlocking, greatest);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.ev_lat, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.done, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.keys_down, hipEventDisableTiming);
@@ -1438,13 +1442,16 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   uint8_t* kho = zk ? (uint8_t*)L.z_keys.p : ho + (verdict && !zc ? n : 0);  // keys on the host
   const bool early = kcb && keys && verdict;
   auto t_k = t_up;
+  // A keyed batch's cache keys: with the image read in place, on the lane's
+  // second stream, beside the verify kernel (the caller's cache walk then
+  // overlaps the verification); the windows are staged in LDS (kind 2).
+  const bool kside = keys && in_place;
+  hipStream_t ks = kside ? L.hstream : L.stream;
   if (keys) {
-    SV_HIP(sv_launch_hash(0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n, d_keys,
-                          L.stream));
-    if (early) {
-      if (!zk) SV_HIP(hipMemcpyAsync(kho, L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, L.stream));
-      SV_HIP(hipEventRecord(L.keys_down, L.stream));
-    }
+    SV_HIP(sv_launch_hash(in_place ? 2 : 0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
+                          d_keys, ks));
+    if (!zk) SV_HIP(hipMemcpyAsync(kho, L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, ks));
+    SV_HIP(hipEventRecord(L.keys_down, ks));
   }
   if (verdict) {
     const int mode = im.var ? 1 : (in.fixed == 32 ? 0 : 2);
@@ -1468,7 +1475,6 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
     t_k = std::chrono::steady_clock::now();
     if (!zc) SV_HIP(hipMemcpyAsync(ho, L.d_out.p, n, hipMemcpyDeviceToHost, L.stream));
   }
-  if (keys && !early && !zk) SV_HIP(hipMemcpyAsync(kho, L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, L.stream));
   SV_HIP(hipEventRecord(L.done, L.stream));
   const auto t_down = std::chrono::steady_clock::now();
   if (early) {
@@ -1480,6 +1486,7 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   lat_build(L);  // (after the verify work: a build waits for it on the device)
   const auto t_b = std::chrono::steady_clock::now();
   SV_HIP(hipEventSynchronize(L.done));
+  if (keys && !early) SV_HIP(hipEventSynchronize(L.keys_down));
   if (verdict) std::memcpy(verdict, vho, n);
   if (keys && !early) std::memcpy(keys, kho, 32 * n);
   if (warm) ++L.warm;
@@ -1505,7 +1512,10 @@ int lat_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* 
   std::lock_guard<std::mutex> g(D.lat.mu);
   SV_HIP(hipSetDevice(D.phys));
   const int rc = lat_slice_locked(D, in, n, verdict, keys, kcb, cb_done);
-  if (rc != SV_OK && D.lat.ready) (void)hipStreamSynchronize(D.lat.stream);  // nothing of this call in flight
+  if (rc != SV_OK && D.lat.ready) {  // nothing of this call in flight
+    (void)hipStreamSynchronize(D.lat.stream);
+    if (D.lat.hstream) (void)hipStreamSynchronize(D.lat.hstream);
+  }
   return rc;
 }
 

@@ -41,6 +41,63 @@ __global__ __launch_bounds__(SV_HBLOCK) void sv_cachekey_kernel(sv_hparams p) {
   }
 }
 
+// Cache keys of a latency-lane batch, whose image the kernel reads in place
+// from mapped host memory: there every dependent round trip costs ~2 us and
+// the per-lane kernel above reads each message dword by dword at a stride of
+// one message per lane (~64 lines per load instruction), which measured
+// ~140 us for 1k SCP envelopes.  Here one wave stages the 16-byte-aligned
+// windows of its 64 messages in LDS first -- item j's window by the whole
+// wave, one 16-byte load per lane, so each load instruction is one contiguous
+// run -- and pk / sig come as 16-byte loads; each lane then hashes its item
+// from LDS (a message longer than the window is read from memory).
+#define SV_KWIN 33  // quads per staged window: a 512-byte message at any alignment
+__global__ __launch_bounds__(64) void sv_cachekey_lds_kernel(sv_hparams p) {
+  __shared__ uint4 s_win[64][SV_KWIN];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t base = (uint64_t)blockIdx.x * 64;
+  const uint64_t last = p.n - 1;
+  SV_NOUNROLL for (uint32_t j = 0; j < 64; ++j) {
+    const uint64_t ij = base + j <= last ? base + j : last;  // (wave-uniform)
+    const uint8_t* m;
+    uint32_t L;
+    sv_item_msg(p, ij, m, L);
+    const uint32_t lead = (uint32_t)((uintptr_t)m & 15u);
+    const uint32_t nq = (lead + L + 15u) >> 4;
+    if (nq <= SV_KWIN && lane < nq) s_win[j][lane] = ((const uint4*)(m - lead))[lane];
+  }
+  // (LDS is in order within the wave)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint64_t i = base + lane;
+  const uint64_t ii = i <= last ? i : last;
+  const uint8_t* m;
+  uint32_t L;
+  sv_item_msg(p, ii, m, L);
+  const uint32_t lead = (uint32_t)((uintptr_t)m & 15u);
+  const bool fits = ((lead + L + 15u) >> 4) <= SV_KWIN;
+  uint32_t pk[8], sig[16];
+  {
+    const uint4* a = (const uint4*)(p.pk + 8 * ii);
+    const uint4* b = (const uint4*)(p.sig + 16 * ii);
+    SV_UNROLL for (int q = 0; q < 2; ++q) {
+      const uint4 v = a[q];
+      pk[4 * q] = v.x; pk[4 * q + 1] = v.y; pk[4 * q + 2] = v.z; pk[4 * q + 3] = v.w;
+    }
+    SV_UNROLL for (int q = 0; q < 4; ++q) {
+      const uint4 v = b[q];
+      sig[4 * q] = v.x; sig[4 * q + 1] = v.y; sig[4 * q + 2] = v.z; sig[4 * q + 3] = v.w;
+    }
+  }
+  uint32_t k[8];
+  sv_cache_key(k, pk, sig, fits ? (const uint8_t*)&s_win[lane][0] + lead : m, L);
+  if (i <= last) {
+    uint4* o = (uint4*)(p.out + 8 * i);
+    o[0] = uint4{k[0], k[1], k[2], k[3]};
+    o[1] = uint4{k[4], k[5], k[6], k[7]};
+  }
+}
+
 __global__ __launch_bounds__(SV_HBLOCK) void sv_sha256_kernel(sv_hparams p) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint8_t* m;
@@ -54,7 +111,9 @@ __global__ __launch_bounds__(SV_HBLOCK) void sv_sha256_kernel(sv_hparams p) {
 
 extern "C" {
 
-// kind 0: cache keys (pk, sig, msg), kind 1: SHA-256 (msg only)
+// kind 0: cache keys (pk, sig, msg), kind 1: SHA-256 (msg only), kind 2: cache
+// keys of an image in mapped host memory (windows staged in LDS; pk and sig
+// 16-byte aligned, out 16-byte aligned)
 hipError_t sv_launch_hash(int kind, unsigned max_blocks, const void* pk, const void* sig, const void* msg,
                           const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n, void* out,
                           hipStream_t s) {
@@ -69,8 +128,13 @@ hipError_t sv_launch_hash(int kind, unsigned max_blocks, const void* pk, const v
   p.out = (uint32_t*)out;
   uint64_t need = (n + SV_HBLOCK - 1) / SV_HBLOCK;
   const unsigned grid = (unsigned)(need < max_blocks ? (need ? need : 1) : max_blocks);
-  if (kind == 0) hipLaunchKernelGGL(sv_cachekey_kernel, dim3(grid), dim3(SV_HBLOCK), 0, s, p);
-  else hipLaunchKernelGGL(sv_sha256_kernel, dim3(grid), dim3(SV_HBLOCK), 0, s, p);
+  if (kind == 2) {
+    if (n) hipLaunchKernelGGL(sv_cachekey_lds_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, p);
+  } else if (kind == 0) {
+    hipLaunchKernelGGL(sv_cachekey_kernel, dim3(grid), dim3(SV_HBLOCK), 0, s, p);
+  } else {
+    hipLaunchKernelGGL(sv_sha256_kernel, dim3(grid), dim3(SV_HBLOCK), 0, s, p);
+  }
   return hipGetLastError();
 }
 
