@@ -56,26 +56,21 @@ __global__ __launch_bounds__(64) void sv_cachekey_lds_kernel(sv_hparams p) {
   const uint32_t lane = threadIdx.x;
   const uint64_t base = (uint64_t)blockIdx.x * 64;
   const uint64_t last = p.n - 1;
-  SV_NOUNROLL for (uint32_t j = 0; j < 64; ++j) {
-    const uint64_t ij = base + j <= last ? base + j : last;  // (wave-uniform)
-    const uint8_t* m;
-    uint32_t L;
-    sv_item_msg(p, ij, m, L);
-    const uint32_t lead = (uint32_t)((uintptr_t)m & 15u);
-    const uint32_t nq = (lead + L + 15u) >> 4;
-    if (nq <= SV_KWIN && lane < nq) s_win[j][lane] = ((const uint4*)(m - lead))[lane];
-  }
-  // (LDS is in order within the wave)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint64_t i = base + lane;
   const uint64_t ii = i <= last ? i : last;
+  // every lane fetches its item's message address first (one load each, in
+  // parallel: the offsets live in the same mapped image, a round trip apiece),
+  // then item j's window is loaded by the whole wave with j's address read
+  // from lane j (v_readlane), by LDS-DMA (global_load_lds_dwordx4: no VGPR
+  // round trip, so the 64 loads are in flight together and cost one wait)
   const uint8_t* m;
   uint32_t L;
   sv_item_msg(p, ii, m, L);
   const uint32_t lead = (uint32_t)((uintptr_t)m & 15u);
-  const bool fits = ((lead + L + 15u) >> 4) <= SV_KWIN;
+  const uint32_t nq = (lead + L + 15u) >> 4;
+  const uint64_t wa = (uint64_t)(uintptr_t)(m - lead);
+  const uint32_t wlo = (uint32_t)wa, whi = (uint32_t)(wa >> 32);
+  // (pk and sig in flight with the windows)
   uint32_t pk[8], sig[16];
   {
     const uint4* a = (const uint4*)(p.pk + 8 * ii);
@@ -89,6 +84,16 @@ __global__ __launch_bounds__(64) void sv_cachekey_lds_kernel(sv_hparams p) {
       sig[4 * q] = v.x; sig[4 * q + 1] = v.y; sig[4 * q + 2] = v.z; sig[4 * q + 3] = v.w;
     }
   }
+  SV_NOUNROLL for (uint32_t j = 0; j < 64; ++j) {
+    const uint32_t nqj = (uint32_t)__builtin_amdgcn_readlane((int)nq, (int)j);
+    const uint64_t aj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)whi, (int)j) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)wlo, (int)j);
+    if (nqj <= SV_KWIN && lane < nqj)
+      __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(aj + 16u * lane),
+                                       (__attribute__((address_space(3))) void*)((char*)&s_win[j][0]), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA'd windows are in LDS)
+  const bool fits = nq <= SV_KWIN;
   uint32_t k[8];
   sv_cache_key(k, pk, sig, fits ? (const uint8_t*)&s_win[lane][0] + lead : m, L);
   if (i <= last) {
