@@ -53,6 +53,9 @@ __global__ __launch_bounds__(SV_HBLOCK) void sv_cachekey_kernel(sv_hparams p) {
 #define SV_KWIN 33  // quads per staged window: a 512-byte message at any alignment
 __global__ __launch_bounds__(64) void sv_cachekey_lds_kernel(sv_hparams p) {
   __shared__ uint4 s_win[64][SV_KWIN];
+  // (the latency lane's verify kernels run at priority 3: at the default
+  // priority these waves would wait out the comb kernel on every shared SIMD)
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t lane = threadIdx.x;
   const uint64_t base = (uint64_t)blockIdx.x * 64;
   const uint64_t last = p.n - 1;
