@@ -222,8 +222,19 @@ void VerifyMicroBatcher::run() {
       }
     }
     bool ok = true;
+    // The engine is free once verifySigBatch returns: the next batch may be
+    // flushed (WhenIdle) while this one's promises and continuations run.
+    bool released = false;
+    auto release = [&] {
+      if (released) return;
+      released = true;
+      std::lock_guard<std::mutex> g(mMu);
+      --mInFlight;
+      if (mPolicy == FlushPolicy::WhenIdle && mQueued.load() > 0) mCv.notify_all();
+    };
     try {
       std::vector<bool> v = PubKeyUtils::verifySigBatch(items);
+      release();
       if (mRecordLatency) {
         const auto now = Clock::now();
         lat.resize(take);
@@ -243,6 +254,7 @@ void VerifyMicroBatcher::run() {
         }
       }
     } catch (...) {  // (only a non-ed25519 key: the reference's releaseAssert)
+      release();
       ok = false;
       for (size_t i = 0; i < take; ++i) {
         if (std::promise<bool>* p = recs[i]->done) {
@@ -259,7 +271,6 @@ void VerifyMicroBatcher::run() {
       }
     }
     lk.lock();
-    --mInFlight;
     ++mStats.batches;
     if (bySize) ++mStats.flushedBySize;
     else if (idle) ++mStats.flushedIdle;
@@ -275,8 +286,6 @@ void VerifyMicroBatcher::run() {
     }
     mCompleted += take;
     mDoneCv.notify_all();
-    // (WhenIdle: items that queued while this batch ran may flush now)
-    if (mPolicy == FlushPolicy::WhenIdle && mQueued.load() > 0) mCv.notify_all();
   }
 }
 
