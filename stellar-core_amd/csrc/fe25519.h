@@ -369,10 +369,16 @@ SV_HD void fe_sq_cm(fe& h, const fe& f) {
 // Device: each product / square as one generated inline-asm
 // statement (fe_asm_gen.h, tools/gen_fe_asm.py), same arithmetic as the
 // column-major forms above.
+// (-DSV_FE_ASM_ON=0: A/B builds only, the column-major forms on the device)
 #if defined(__HIP_DEVICE_COMPILE__)
+#ifndef SV_FE_ASM_ON
 #define SV_FE_ASM_ON 1
+#endif
+#if SV_FE_ASM_ON
 #include "fe_asm_gen.h"
+#endif
 #else
+#undef SV_FE_ASM_ON
 #define SV_FE_ASM_ON 0
 #endif
 
