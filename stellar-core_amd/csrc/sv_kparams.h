@@ -73,9 +73,25 @@ __device__ __forceinline__ void sv_load_and_hash_lds(const sv_kparams& p, uint64
   const uint32_t lead = (uint32_t)((uintptr_t)mp & 15u);
   const uint32_t nq = (lead + mlen + 15u) >> 4;
   const bool fits = nq <= SV_MSG_CAP / 16;
-  if (fits) {
+  if (fits && nq > 0) {
+    // every load of the window first (unpredicated: an index past the window
+    // re-reads its last quad), then the LDS writes: a load-then-write loop
+    // waits out one round trip per iteration (up to SV_MSG_CAP / 16 / LPS of
+    // them, ~2 us each from mapped host memory)
     const sv_u4* src = (const sv_u4*)(mp - lead);
-    for (uint32_t c = li; c < nq; c += LPS) lbuf[c] = src[c];
+    constexpr int kIt = (SV_MSG_CAP / 16 + LPS - 1) / LPS;
+    sv_u4 t[kIt];
+    SV_UNROLL for (int k = 0; k < kIt; ++k) {
+      const uint32_t c = li + (uint32_t)(k * LPS);
+      t[k] = src[c < nq ? c : nq - 1];
+    }
+    // (pins the loads here: LLVM would otherwise sink each one into its
+    // predicated LDS write below, one round trip apiece again)
+    SV_UNROLL for (int k = 0; k < kIt; ++k) asm volatile("" : "+v"(t[k].x), "+v"(t[k].y), "+v"(t[k].z), "+v"(t[k].w));
+    SV_UNROLL for (int k = 0; k < kIt; ++k) {
+      const uint32_t c = li + (uint32_t)(k * LPS);
+      if (c < nq) lbuf[c] = t[k];
+    }
   }
   // (the lanes of one wave: LDS is in order within the wave)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
