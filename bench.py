@@ -417,7 +417,8 @@ def scp_latency_set(sodium, n=1000, adversarial=0.1, seed=20250211):
 
 class ScpParams(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint32) for k in ("struct_size", "producers", "burst", "interval_us", "max_batch",
-                                               "max_delay_us", "workers", "policy", "linger_us", "idle_in_flight")]
+                                               "max_delay_us", "workers", "policy", "linger_us", "idle_in_flight",
+                                               "quiet_us", "max_linger_us")]
 
 
 class ScpResult(ctypes.Structure):
@@ -429,7 +430,8 @@ class ScpResult(ctypes.Structure):
                                                   "max_batch")]
                 + [("mean_batch", ctypes.c_double)]
                 + [(k, ctypes.c_uint64) for k in ("gpu_batches", "gpu_signatures", "cpu_signatures", "fallbacks")]
-                + [(k, ctypes.c_double) for k in ("wall_s", "ready_p50_us", "ready_p99_us")])
+                + [(k, ctypes.c_double) for k in ("wall_s", "ready_p50_us", "ready_p99_us")]
+                + [("burst_waits", ctypes.c_uint64)])
 
 
 def scp_envelope_set(sodium, n, seed, adversarial=0.1, validators=100):
@@ -516,11 +518,11 @@ def config4_integrated(sv, sodium, n=48000):
     gen_s = time.perf_counter() - t0
 
     def run(sl, producers, burst, interval_us, workers=2, policy=0, linger_us=0, max_batch=8192,
-            max_delay_us=2000):
+            max_delay_us=2000, quiet_us=10, max_linger_us=200):
         a, b = sl
         m = b - a
         p = ScpParams(ctypes.sizeof(ScpParams), producers, burst, interval_us, max_batch, max_delay_us, workers,
-                      policy, linger_us, 1)
+                      policy, linger_us, 1, quiet_us, max_linger_us)
         r = ScpResult()
         out = np.full(m, 7, np.uint8)
         o0 = int(off[a])
@@ -537,6 +539,7 @@ def config4_integrated(sv, sodium, n=48000):
                 d[k.replace("_us", "_ms")] = d.pop(k) / 1e3
         d.update({"envelopes": m, "producers": producers, "burst": burst, "interval_us": interval_us,
                   "workers": workers, "policy": "deadline" if policy else "when_idle", "linger_us": linger_us,
+                  "quiet_us": quiet_us, "max_linger_us": max_linger_us,
                   "max_batch_setting": max_batch, "max_delay_us": max_delay_us,
                   "offered_per_s": (burst * 1e6 / interval_us) if interval_us else None,
                   "achieved_per_s": m / d["wall_s"] if d["wall_s"] > 0 else None,
@@ -549,7 +552,7 @@ def config4_integrated(sv, sodium, n=48000):
     run((0, 2000), 4, 1000, 5000)  # warm-up: lane, staging and the validators' device key tables
     sv.key_cache_wait(0)
     res["paced_1k_every_5ms"] = run((2000, 32000), 4, 1000, 5000)
-    res["paced_1k_every_5ms_linger_50us"] = run((2000, 32000), 4, 1000, 5000, linger_us=50)
+    res["paced_1k_every_5ms_no_burst_wait"] = run((2000, 32000), 4, 1000, 5000, quiet_us=0)
     res["trickle_4_every_200us"] = run((32000, 36000), 4, 4, 200)
     res["flood"] = run((0, n), 4, 0, 0, workers=4)
     res["paced_1k_every_5ms_deadline_policy"] = run((36000, 46000), 4, 1000, 5000, policy=1)

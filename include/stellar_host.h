@@ -221,6 +221,7 @@ typedef struct svh_scp_params {
   uint32_t producers, burst, interval_us;
   uint32_t max_batch, max_delay_us, workers;
   uint32_t policy, linger_us, idle_in_flight;
+  uint32_t quiet_us, max_linger_us; /* WhenIdle burst wait (VerifyMicroBatcher::Options; quiet 0: off) */
 } svh_scp_params;
 typedef struct svh_scp_result {
   double verdict_p50_us, verdict_p90_us, verdict_p99_us, verdict_max_us, verdict_mean_us; /* submit -> continuation */
@@ -232,6 +233,7 @@ typedef struct svh_scp_result {
   uint64_t gpu_batches, gpu_signatures, cpu_signatures, fallbacks; /* engine counts over the run */
   double wall_s; /* first submission -> last main-thread verifySig */
   double ready_p50_us, ready_p99_us; /* submit -> the item's batch verified and cached (before its continuations) */
+  uint64_t burst_waits;              /* idle flushes that first waited for a burst to end */
 } svh_scp_result;
 int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                 const uint32_t* msg_len, size_t n, const svh_scp_params* params, uint8_t* verdict,

@@ -21,7 +21,9 @@ VerifyMicroBatcher::VerifyMicroBatcher(Options const& o)
       mRecordLatency(o.recordLatency),
       mPolicy(o.policy),
       mIdleInFlight(std::max(1u, o.idleInFlight)),
-      mLinger(std::min(o.linger, o.maxDelay)) {
+      mLinger(std::min(o.linger, o.maxDelay)),
+      mQuiet(o.quiet),
+      mMaxLinger(std::min(o.maxLinger, o.maxDelay)) {
   const unsigned w = std::max(1u, o.workers);
   mWorkers.reserve(w);
   for (unsigned i = 0; i < w; ++i) mWorkers.emplace_back([this] { run(); });
@@ -74,6 +76,7 @@ void VerifyMicroBatcher::enqueue(PublicKey const& key, ByteSlice const& sig, Byt
   r.cb = cb;
   if (mRecordLatency) r.t0 = Clock::now();
   r.arrivalNs = nowNs();
+  mNewestNs.store(r.arrivalNs, std::memory_order_relaxed);
   size_t q;
   {
     Shard& sh = mShards[tShard];
@@ -183,6 +186,24 @@ void VerifyMicroBatcher::run() {
           mCv.wait_for(lk, std::chrono::nanoseconds(lingerEnd - now),
                        [&] { return mStop || mQueued.load() >= mMaxBatch; });
           continue;
+        }
+        if (mQuiet.count() > 0 && mQueued.load() > 1) {
+          // a burst: wait (unlocked, yielding) until it has been quiet for
+          // mQuiet, the oldest item is mMaxLinger old, or a batch is full
+          const int64_t cap = std::min(oldest + (int64_t)mMaxLinger.count() * 1000, deadline);
+          const int64_t q = (int64_t)mQuiet.count() * 1000;
+          if (now < cap && now - mNewestNs.load(std::memory_order_relaxed) < q) {
+            lk.unlock();
+            for (;;) {
+              const int64_t t = nowNs();
+              if (t >= cap || t - mNewestNs.load(std::memory_order_relaxed) >= q || mQueued.load() >= mMaxBatch)
+                break;
+              std::this_thread::yield();
+            }
+            lk.lock();
+            ++mStats.burstWaits;
+            continue;  // (re-evaluate: another worker may have flushed meanwhile)
+          }
         }
         idle = now < deadline;
       } else if (now < deadline) {

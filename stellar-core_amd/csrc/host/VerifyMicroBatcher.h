@@ -67,6 +67,15 @@ class VerifyMicroBatcher {
     unsigned idleInFlight = 1;
     // WhenIdle: an idle flush waits until the oldest item is this old
     std::chrono::microseconds linger{0};
+    // WhenIdle: while a burst is arriving (more than one item queued and the
+    // newest less than `quiet` old) an idle flush waits for the burst to end,
+    // at most until the oldest item is `maxLinger` old, so a burst becomes one
+    // batch instead of a small first batch that the rest queues behind.  A
+    // lone item is flushed at once.  0 disables.  (The wait is a yield loop
+    // without the queue lock: a condition-variable timeout this short
+    // oversleeps by the timer slack.)
+    std::chrono::microseconds quiet{10};
+    std::chrono::microseconds maxLinger{200};
   };
   explicit VerifyMicroBatcher(Options const& opts);
   VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay, unsigned workers = 2,
@@ -97,6 +106,7 @@ class VerifyMicroBatcher {
     uint64_t flushedBySize = 0;
     uint64_t flushedByDeadline = 0;
     uint64_t flushedIdle = 0;  // WhenIdle: below maxBatch, before the deadline, engine idle
+    uint64_t burstWaits = 0;   // WhenIdle: idle flushes that first waited for a burst to end (quiet)
     uint64_t maxBatchSeen = 0;
   };
   Stats stats() const;
@@ -141,6 +151,8 @@ class VerifyMicroBatcher {
   const FlushPolicy mPolicy;
   const unsigned mIdleInFlight;
   const std::chrono::microseconds mLinger;
+  const std::chrono::microseconds mQuiet, mMaxLinger;
+  std::atomic<int64_t> mNewestNs{0};  // arrival of the newest queued item (a hint: WhenIdle's quiet period)
   unsigned mInFlight = 0;  // batches being verified (under mMu)
   Shard mShards[kShards];
   std::atomic<size_t> mQueued{0};

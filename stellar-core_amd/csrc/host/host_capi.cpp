@@ -448,6 +448,8 @@ int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
     o.policy = prm->policy == 1 ? VerifyMicroBatcher::FlushPolicy::Deadline : VerifyMicroBatcher::FlushPolicy::WhenIdle;
     o.idleInFlight = std::max(1u, prm->idle_in_flight);
     o.linger = std::chrono::microseconds(prm->linger_us);
+    o.quiet = std::chrono::microseconds(prm->quiet_us);
+    o.maxLinger = std::chrono::microseconds(prm->max_linger_us);
     o.recordLatency = true;  // (submit -> the batch's verdicts are in the cache, before its continuations run)
     std::vector<Clk::time_point> tSub(n), tVer(n), tMain(n);
     std::vector<uint8_t> cbVerdict(n, 2);
@@ -560,6 +562,7 @@ int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
     res->flushed_by_deadline = st.flushedByDeadline;
     res->flushed_idle = st.flushedIdle;
     res->max_batch = st.maxBatchSeen;
+    res->burst_waits = st.burstWaits;
     res->mean_batch = st.batches ? (double)st.items / (double)st.batches : 0;
     res->gpu_batches = eng.gpuBatches;
     res->gpu_signatures = eng.gpuSignatures;

@@ -492,7 +492,8 @@ def test_micro_batcher_multiple_workers(host, engine, golden):
 
 class ScpParams(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint32) for k in ("struct_size", "producers", "burst", "interval_us", "max_batch",
-                                               "max_delay_us", "workers", "policy", "linger_us", "idle_in_flight")]
+                                               "max_delay_us", "workers", "policy", "linger_us", "idle_in_flight",
+                                               "quiet_us", "max_linger_us")]
 
 
 class ScpResult(ctypes.Structure):
@@ -504,11 +505,12 @@ class ScpResult(ctypes.Structure):
                                                   "max_batch")]
                 + [("mean_batch", ctypes.c_double)]
                 + [(k, ctypes.c_uint64) for k in ("gpu_batches", "gpu_signatures", "cpu_signatures", "fallbacks")]
-                + [(k, ctypes.c_double) for k in ("wall_s", "ready_p50_us", "ready_p99_us")])
+                + [(k, ctypes.c_double) for k in ("wall_s", "ready_p50_us", "ready_p99_us")]
+                + [("burst_waits", ctypes.c_uint64)])
 
 
 def scp_run(host, d, rows, producers, burst, interval_us, max_batch=8192, max_delay_us=2000, workers=2, policy=0,
-            linger_us=0):
+            linger_us=0, quiet_us=0, max_linger_us=0):
     """svh_scp_run (config 4 through the micro-batcher: continuation submits,
     a main thread calling verifySig per envelope) over golden rows."""
     n = len(rows)
@@ -519,7 +521,7 @@ def scp_run(host, d, rows, producers, burst, interval_us, max_batch=8192, max_de
     msg = np.ascontiguousarray(d["msg"])
     out = np.full(n, 7, np.uint8)
     p = ScpParams(ctypes.sizeof(ScpParams), producers, burst, interval_us, max_batch, max_delay_us, workers, policy,
-                  linger_us, 1)
+                  linger_us, 1, quiet_us, max_linger_us)
     r = ScpResult()
     vp = ctypes.c_void_p
     rc = host.svh_scp_run(vp(pk.ctypes.data), vp(sig.ctypes.data), vp(msg.ctypes.data), vp(off.ctypes.data),
@@ -585,6 +587,21 @@ def test_scp_run_linger_collects_a_burst(host, engine, golden):
     out, r = scp_run(host, d, rows, producers=1, burst=32, interval_us=0, max_delay_us=400_000, linger_us=200_000)
     assert (out == 1).all() and r.main_hits == len(rows)
     assert r.batches == 1 and r.max_batch == 32
+
+
+def test_scp_run_quiet_period_makes_one_batch_per_burst(host, engine, golden):
+    """WhenIdle with a quiet period: a burst that is still arriving is waited
+    for (until it has been quiet for quiet_us) and flushed as ONE batch; lone
+    items still go at once."""
+    d = golden["valid"]
+    rows = np.arange(96)
+    out, r = scp_run(host, d, rows, producers=1, burst=32, interval_us=60_000, max_delay_us=400_000,
+                     quiet_us=20_000, max_linger_us=300_000)
+    assert (out == 1).all() and r.main_hits == len(rows)
+    assert r.batches == 3 and r.max_batch == 32 and r.burst_waits >= 1
+    out, r = scp_run(host, d, rows[:6], producers=1, burst=1, interval_us=5000, max_delay_us=400_000,
+                     quiet_us=20_000, max_linger_us=300_000)
+    assert (out == 1).all() and r.batches == 6 and r.burst_waits == 0
 
 
 @pytest.mark.gpu

@@ -4,7 +4,8 @@ bench's config4_integrated) over a grid of micro-batcher settings, one JSON
 line per setting: submit -> batch verified (ready), -> continuation
 (verdict) and -> main-thread verifySig latencies, batch counts.
 
-  python tools/scp_probe.py [n] [settings]   settings: "burst:interval:linger:inflight:workers:producers,..."
+  python tools/scp_probe.py [n] [settings]
+    settings: "burst:interval:linger:inflight:workers:producers[:quiet:maxlinger],..." (quiet default 10 us)
 With SV_HOST_TRACE=1 / SV_LAT_TRACE=1 in the environment the engine prints
 its per-batch host stages to stderr."""
 import ctypes
@@ -33,9 +34,10 @@ def main():
     host.svh_scp_run.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                                          ctypes.c_void_p]
     for k, spec in enumerate(["1000:5000:0:1:2:4"] + grid.split(",")):
-        burst, interval, linger, inflight, workers, producers = (int(x) for x in spec.split(":"))
+        v = [int(x) for x in spec.split(":")] + [10, 200][len(spec.split(":")) - 6:]
+        burst, interval, linger, inflight, workers, producers, quiet, maxl = v[:8]
         p = bench.ScpParams(ctypes.sizeof(bench.ScpParams), producers, burst, interval, 8192, 2000, workers, 0, linger,
-                            inflight)
+                            inflight, quiet, maxl)
         r = bench.ScpResult()
         out = np.full(n, 7, np.uint8)
         host.svh_cache_clear()
