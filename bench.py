@@ -518,7 +518,7 @@ def config4_integrated(sv, sodium, n=48000):
     gen_s = time.perf_counter() - t0
 
     def run(sl, producers, burst, interval_us, workers=2, policy=0, linger_us=0, max_batch=8192,
-            max_delay_us=2000, quiet_us=10, max_linger_us=200):
+            max_delay_us=2000, quiet_us=0, max_linger_us=200):
         a, b = sl
         m = b - a
         p = ScpParams(ctypes.sizeof(ScpParams), producers, burst, interval_us, max_batch, max_delay_us, workers,
@@ -552,7 +552,7 @@ def config4_integrated(sv, sodium, n=48000):
     run((0, 2000), 4, 1000, 5000)  # warm-up: lane, staging and the validators' device key tables
     sv.key_cache_wait(0)
     res["paced_1k_every_5ms"] = run((2000, 32000), 4, 1000, 5000)
-    res["paced_1k_every_5ms_no_burst_wait"] = run((2000, 32000), 4, 1000, 5000, quiet_us=0)
+    res["paced_1k_every_5ms_burst_wait_20us"] = run((2000, 32000), 4, 1000, 5000, quiet_us=20, max_linger_us=300)
     res["trickle_4_every_200us"] = run((32000, 36000), 4, 4, 200)
     res["flood"] = run((0, n), 4, 0, 0, workers=4)
     res["paced_1k_every_5ms_deadline_policy"] = run((36000, 46000), 4, 1000, 5000, policy=1)

@@ -5,7 +5,7 @@ line per setting: submit -> batch verified (ready), -> continuation
 (verdict) and -> main-thread verifySig latencies, batch counts.
 
   python tools/scp_probe.py [n] [settings]
-    settings: "burst:interval:linger:inflight:workers:producers[:quiet:maxlinger],..." (quiet default 10 us)
+    settings: "burst:interval:linger:inflight:workers:producers[:quiet:maxlinger],..." (quiet default 0: off)
 With SV_HOST_TRACE=1 / SV_LAT_TRACE=1 in the environment the engine prints
 its per-batch host stages to stderr."""
 import ctypes
@@ -34,7 +34,7 @@ def main():
     host.svh_scp_run.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                                          ctypes.c_void_p]
     for k, spec in enumerate(["1000:5000:0:1:2:4"] + grid.split(",")):
-        v = [int(x) for x in spec.split(":")] + [10, 200][len(spec.split(":")) - 6:]
+        v = [int(x) for x in spec.split(":")] + [0, 200][len(spec.split(":")) - 6:]
         burst, interval, linger, inflight, workers, producers, quiet, maxl = v[:8]
         p = bench.ScpParams(ctypes.sizeof(bench.ScpParams), producers, burst, interval, 8192, 2000, workers, 0, linger,
                             inflight, quiet, maxl)
