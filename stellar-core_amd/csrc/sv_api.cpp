@@ -179,6 +179,7 @@ struct Stage {
   std::vector<hipEvent_t> pev;  // keys of piece k are down (one-chunk keyed batches)
   bool busy = false;  // a chunk's D2H is pending on `down`
   size_t lo = 0, m = 0;
+  const uint8_t* zv = nullptr;  // the chunk's verdicts in mapped memory (written in place), else in h_out
 };
 
 // Latency lane of a slot.  Batches that take the latency kernels (one staging
@@ -249,7 +250,8 @@ struct Device {
   hipEvent_t dep_in = nullptr, dep_out = nullptr;
   std::mutex mu;
   Stage st[2];
-  HostBuf z_in;  // mapped: a one-chunk batch's image, read in place (bulk_in_place)
+  HostBuf z_in;   // mapped: a one-chunk batch's image, read in place (bulk_in_place)
+  HostBuf z_out;  // mapped: its verdicts, written in place (bulk_zc_out)
   DevBuf msg, off, len, keys;  // sha256 batches
   HostBuf h_sha;
   // timing
@@ -350,7 +352,7 @@ int init_device(Device& D) {
   SV_HIP(hipStreamCreateWithFlags(&D.d2h, hipStreamNonBlocking));
   SV_HIP(hipEventCreateWithFlags(&D.dep_in, hipEventDisableTiming));
   SV_HIP(hipEventCreateWithFlags(&D.dep_out, hipEventDisableTiming));
-  D.z_in.mapped = true;
+  D.z_in.mapped = D.z_out.mapped = true;
   for (Stage& s : D.st) {
     SV_HIP(hipEventCreateWithFlags(&s.up, hipEventDisableTiming));
     SV_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
@@ -378,6 +380,7 @@ void release_device(Device& D) {
   D.pending.clear();
   D.pending_n.clear();
   D.z_in.release();
+  D.z_out.release();
   for (Stage& s : D.st) {
     s.h_in.release(); s.h_out.release();
     s.d_in.release(); s.d_verdict.release(); s.d_keys.release();
@@ -503,6 +506,12 @@ size_t share_upload_bytes() {
 // chunk's kernels and stays staged).
 bool bulk_in_place() {
   static const bool b = env_size("SV_BULK_ZC_IN", 1) != 0;
+  return b;
+}
+// ... and their verdicts are written in place too (SV_BULK_ZC_OUT, default on):
+// the kernels store them to mapped memory, so no copy is queued behind them.
+bool bulk_zc_out() {
+  static const bool b = env_size("SV_BULK_ZC_OUT", 1) != 0;
   return b;
 }
 bool share_now(const Device& D) {
@@ -796,9 +805,10 @@ double trace_abs_us() {
 int drain_stage(Stage& s, uint8_t* verdict, uint8_t* keys) {
   if (!s.busy) return SV_OK;
   SV_HIP(hipEventSynchronize(s.down));
+  if (stage_trace()) fprintf(stderr, "SV_STAGE_TRACE down synced @%.1f\n", trace_abs_us());
   s.busy = false;
   const uint8_t* h = (const uint8_t*)s.h_out.p;
-  if (verdict) std::memcpy(verdict + s.lo, h, s.m);
+  if (verdict) std::memcpy(verdict + s.lo, s.zv ? s.zv : h, s.m);
   if (keys) std::memcpy(keys + 32 * s.lo, h + (verdict ? s.m : 0), 32 * s.m);
   return SV_OK;
 }
@@ -967,11 +977,13 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     const std::vector<size_t> pb = early ? key_pieces(m) : std::vector<size_t>{0, m};
     const size_t P = pb.size() - 1;
     const bool in_place = single && P == 1 && bulk_in_place();
+    const bool zc_out = in_place && verdict && bulk_zc_out();
     HostBuf& hin = in_place ? D.z_in : s.h_in;
     if ((rc = hin.ensure(im.bytes)) || (!in_place && (rc = s.d_in.ensure(im.bytes))) ||
         (rc = s.h_out.ensure(out_per * m)))
       return rc;
-    if (verdict && (rc = s.d_verdict.ensure(m))) return rc;
+    if (verdict && !zc_out && (rc = s.d_verdict.ensure(m))) return rc;
+    if (zc_out && (rc = D.z_out.ensure(m))) return rc;
     if (keys && (rc = s.d_keys.ensure(32 * m))) return rc;
     uint8_t* d = (uint8_t*)(in_place ? D.z_in.dp : s.d_in.p);
     uint8_t* hp = (uint8_t*)hin.p;
@@ -1054,10 +1066,13 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
     if (stage_trace()) g_trace_pack_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_pack).count();
     if (verdict) {
       const int mode = im.var ? 1 : (in.fixed == 32 ? 0 : 2);
+      // (only the one-lane geometry uses the tables: a quad-geometry batch
+      // skips the key sample, ~4k scattered reads of the caller's keys)
       if (tables < 0)
-        tables = resolve_path(path, chunk) != SV_PATH_LATENCY && (ktm == 1 || (ktm == 2 && repeated_keys(in, n)));
+        tables = launch_geometry(resolve_path(path, chunk), chunk) == SV_PATH_THROUGHPUT &&
+                 (ktm == 1 || (ktm == 2 && repeated_keys(in, n)));
       if ((rc = launch_locked(D, mode, path, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m,
-                              s.d_verdict.p, nullptr, tables != 0)))
+                              zc_out ? D.z_out.dp : s.d_verdict.p, nullptr, tables != 0)))
         return rc;
       trace_at("launched");
     }
@@ -1066,13 +1081,14 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
       SV_HIP(hipStreamWaitEvent(D.d2h, s.done, 0));
     }
     uint8_t* ho = (uint8_t*)s.h_out.p;
-    if (verdict) SV_HIP(hipMemcpyAsync(ho, s.d_verdict.p, m, hipMemcpyDeviceToHost, down_s));
+    if (verdict && !zc_out) SV_HIP(hipMemcpyAsync(ho, s.d_verdict.p, m, hipMemcpyDeviceToHost, down_s));
     if (keys && !early)
       SV_HIP(hipMemcpyAsync(ho + (verdict ? m : 0), s.d_keys.p, 32 * m, hipMemcpyDeviceToHost, down_s));
     SV_HIP(hipEventRecord(s.down, down_s));
     s.busy = true;
     s.lo = lo;
     s.m = m;
+    s.zv = zc_out ? (const uint8_t*)D.z_out.p : nullptr;
     if (early) {
       if (P == 1) {
         SV_HIP(hipEventSynchronize(s.pev[0]));
