@@ -32,6 +32,7 @@
 #include <array>
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <vector>
 
@@ -70,6 +71,13 @@ class Signature {
       if (n == kMax) throw std::length_error("Signature: more than 64 bytes (XDR opaque<64>)");
       buf_[n++] = (uint8_t)*it;
     }
+    n_ = (uint8_t)n;
+  }
+  // (bytes: one copy instead of the iterator loop)
+  void assign(const uint8_t* first, const uint8_t* last) {
+    const size_t n = (size_t)(last - first);
+    if (n > kMax) throw std::length_error("Signature: more than 64 bytes (XDR opaque<64>)");
+    if (n) std::memcpy(buf_, first, n);
     n_ = (uint8_t)n;
   }
   void resize(size_t n) {

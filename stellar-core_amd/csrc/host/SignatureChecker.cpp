@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <exception>
+#include <mutex>
 #include <thread>
 
 #include "HostPool.h"
@@ -212,19 +214,24 @@ void SignatureBatchPrefetch::add(Hash const& contentsHash, std::vector<Decorated
   enumerate(st_, contentsHash, signatures, signers);
 }
 
-void SignatureBatchPrefetch::addBatch(std::vector<TxRef> const& txs) {
+void SignatureBatchPrefetch::addBatch(std::vector<TxRef> const& txs, std::function<void(size_t)> const& prepare) {
   const size_t ntx = txs.size();
   if (txBegin_.empty()) txBegin_.push_back((uint32_t)len_.size());
   constexpr size_t kGrain = 256;
   constexpr size_t kMaxParts = 16;
   const size_t parts = std::min(kMaxParts, std::max<size_t>(1, ntx / kGrain));
   if (parts == 1) {
-    for (auto const& t : txs) {
-      enumerate(st_, *t.contentsHash, *t.signatures, *t.signers);
+    for (size_t k = 0; k < ntx; ++k) {
+      if (prepare) prepare(k);
+      enumerate(st_, *txs[k].contentsHash, *txs[k].signatures, *txs[k].signers);
       txBegin_.push_back((uint32_t)len_.size());
     }
     return;
   }
+  // (an exception must not leave a pool thread: the first is kept and
+  // rethrown on this thread after the loop)
+  std::exception_ptr failed;
+  std::mutex failMu;
   // phase 1: each part enumerates its range of txs into scratch of its own
   // (kept per part across calls: no fresh page faults), recording the pair
   // count after each tx; phase 2: the parts are copied into place in order.
@@ -240,12 +247,19 @@ void SignatureBatchPrefetch::addBatch(std::vector<TxRef> const& txs) {
       s.clear();
       const size_t t0 = ntx * p / parts, t1 = ntx * (p + 1) / parts;
       ends[p].clear();
-      for (size_t t = t0; t < t1; ++t) {
-        enumerate(s, *txs[t].contentsHash, *txs[t].signatures, *txs[t].signers);
-        ends[p].push_back((uint32_t)s.len.size());
+      try {
+        for (size_t t = t0; t < t1; ++t) {
+          if (prepare) prepare(t);
+          enumerate(s, *txs[t].contentsHash, *txs[t].signatures, *txs[t].signers);
+          ends[p].push_back((uint32_t)s.len.size());
+        }
+      } catch (...) {
+        std::lock_guard<std::mutex> g(failMu);
+        if (!failed) failed = std::current_exception();
       }
     }
   });
+  if (failed) std::rethrow_exception(failed);
   std::vector<size_t> pairBase(parts + 1), msgBase(parts + 1);
   pairBase[0] = len_.size();
   msgBase[0] = msg_.size();

@@ -24,6 +24,9 @@
 
 #include <array>
 #include <cstdint>
+#include <functional>
+#include <memory>
+#include <utility>
 #include <vector>
 
 #include "PubKeyUtils.h"
@@ -89,7 +92,12 @@ class SignatureBatchPrefetch {
     std::vector<DecoratedSignature> const* signatures;
     std::vector<Signer> const* signers;
   };
-  void addBatch(std::vector<TxRef> const& txs);
+  // prepare (optional): called as prepare(k) for batch tx k on the thread that
+  // enumerates it, just before, to build the tx's objects in place (the
+  // tx-set entry point marshals its C structs there: one pass over each tx,
+  // its objects still in that core's cache).  An exception thrown by it is
+  // rethrown here once every part has finished.
+  void addBatch(std::vector<TxRef> const& txs, std::function<void(size_t)> const& prepare = {});
   // One engine batch over everything added.  seedCache = false: the verdicts
   // go to the side table only (the engine is called directly, no cache
   // interaction); true: through PubKeyUtils::verifySigBatch, which also fills
@@ -106,10 +114,32 @@ class SignatureBatchPrefetch {
   void buildTable();
   static constexpr size_t kAsyncTableMin = 4096;
   static uint64_t hashOf(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, size_t len);
+  // (growth without zero-filling: every byte of the pair arrays is written
+  // right after the resize that makes room for it)
+  template <typename T>
+  struct NoInit : std::allocator<T> {
+    template <typename U>
+    struct rebind {
+      using other = NoInit<U>;
+    };
+    NoInit() = default;
+    template <typename U>
+    NoInit(NoInit<U> const&) {}
+    template <typename U>
+    void construct(U* p) {
+      ::new ((void*)p) U;
+    }
+    template <typename U, typename... A>
+    void construct(U* p, A&&... a) {
+      ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+  };
+  template <typename T>
+  using RawVec = std::vector<T, NoInit<T>>;
   struct Storage {
-    std::vector<uint8_t> pk, sig, msg;
-    std::vector<uint64_t> off;
-    std::vector<uint32_t> len;
+    RawVec<uint8_t> pk, sig, msg;
+    RawVec<uint64_t> off;
+    RawVec<uint32_t> len;
     std::vector<uint8_t> verdict;
     std::vector<uint32_t> table;    // open addressing: pair index + 1, 0 = empty
     std::vector<uint32_t> txBegin;  // addBatch: first pair of batch tx k (k + 1 entries)
@@ -119,11 +149,11 @@ class SignatureBatchPrefetch {
                         std::vector<Signer> const& signers);
   static Storage& spare();
   Storage st_;
-  std::vector<uint8_t>& pk_ = st_.pk;
-  std::vector<uint8_t>& sig_ = st_.sig;
-  std::vector<uint8_t>& msg_ = st_.msg;
-  std::vector<uint64_t>& off_ = st_.off;
-  std::vector<uint32_t>& len_ = st_.len;
+  RawVec<uint8_t>& pk_ = st_.pk;
+  RawVec<uint8_t>& sig_ = st_.sig;
+  RawVec<uint8_t>& msg_ = st_.msg;
+  RawVec<uint64_t>& off_ = st_.off;
+  RawVec<uint32_t>& len_ = st_.len;
   std::vector<uint8_t>& verdict_ = st_.verdict;
   std::vector<uint32_t>& table_ = st_.table;
   std::vector<uint32_t>& txBegin_ = st_.txBegin;

@@ -67,28 +67,28 @@ void parallelOrThrow(size_t n, size_t grain, std::function<void(size_t, size_t)>
   if (first) std::rethrow_exception(first);
 }
 
-DecoratedSignature decorated(svh_decorated_sig const& s) {
+// (in place: the tx-set marshal builds ~30k of each per call)
+void decoratedInto(DecoratedSignature& d, svh_decorated_sig const& s) {
   if (s.sig_len > 64) throw std::invalid_argument("signature longer than 64 bytes");
-  DecoratedSignature d;
   std::memcpy(d.hint.data(), s.hint, 4);
   d.signature.assign(s.sig, s.sig + s.sig_len);
-  return d;
 }
-
-Signer signer(svh_signer const& s) {
+void signerInto(Signer& g, svh_signer const& s) {
   if (s.type > 3 || s.payload_len > 64) throw std::invalid_argument("bad signer");
-  Signer g;
   g.key.type = (SignerKeyType)s.type;
   std::memcpy(g.key.key.data(), s.key, 32);
   g.key.payload.assign(s.payload, s.payload + s.payload_len);
   g.weight = s.weight;
+}
+Signer signer(svh_signer const& s) {
+  Signer g;
+  signerInto(g, s);
   return g;
 }
 
 std::vector<DecoratedSignature> sigRange(const svh_decorated_sig* sigs, uint32_t off, uint32_t n) {
-  std::vector<DecoratedSignature> v;
-  v.reserve(n);
-  for (uint32_t k = 0; k < n; ++k) v.push_back(decorated(sigs[off + k]));
+  std::vector<DecoratedSignature> v(n);
+  for (uint32_t k = 0; k < n; ++k) decoratedInto(v[k], sigs[off + k]);
   return v;
 }
 
@@ -246,26 +246,33 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
     std::vector<Hash> hashes(ntx);
     std::vector<std::vector<DecoratedSignature>> dsigs(ntx);
     std::vector<std::vector<Signer>> sgn(ntx);
-    // (the C structs -> the mirror's C++ objects, in parallel: a node already
-    // holds these objects; the tx set is independent per tx from here on)
-    parallelOrThrow(ntx, 256, [&](size_t a, size_t b) {
-      for (size_t t = a; t < b; ++t) {
-        std::memcpy(hashes[t].data(), txs[t].contents_hash, 32);
-        dsigs[t] = sigRange(sigs, txs[t].sig_off, txs[t].nsigs);
-        sgn[t].reserve(txs[t].nsigners);
-        for (uint32_t k = 0; k < txs[t].nsigners; ++k) sgn[t].push_back(signer(signers[txs[t].signer_off + k]));
-      }
-    });
+    // the C structs -> the mirror's C++ objects (a node already holds these
+    // objects; the tx set is independent per tx from here on)
+    auto marshal = [&](size_t t) {
+      std::memcpy(hashes[t].data(), txs[t].contents_hash, 32);
+      dsigs[t].resize(txs[t].nsigs);
+      for (uint32_t k = 0; k < txs[t].nsigs; ++k) decoratedInto(dsigs[t][k], sigs[txs[t].sig_off + k]);
+      sgn[t].resize(txs[t].nsigners);
+      for (uint32_t k = 0; k < txs[t].nsigners; ++k) signerInto(sgn[t][k], signers[txs[t].signer_off + k]);
+    };
     double ph[4] = {0, 0, 0, 0};
-    ph[0] = pc.lap("txset: marshal");
     SignatureBatchPrefetch pre;
     if (use_prefetch) {
+      // with the pre-pass each tx is marshalled by the pool thread that
+      // enumerates its pairs, just before (one parallel pass; phase 0 is
+      // then only the allocation, phase 1 both)
       std::vector<SignatureBatchPrefetch::TxRef> refs(ntx);
       for (size_t t = 0; t < ntx; ++t) refs[t] = {&hashes[t], &dsigs[t], &sgn[t]};
-      pre.addBatch(refs);
-      ph[1] = pc.lap("txset: prefetch add");
+      ph[0] = pc.lap("txset: marshal (alloc)");
+      pre.addBatch(refs, marshal);
+      ph[1] = pc.lap("txset: marshal + prefetch add");
       pre.run(use_prefetch == 2);
       ph[2] = pc.lap("txset: prefetch run");
+    } else {
+      parallelOrThrow(ntx, 256, [&](size_t a, size_t b) {
+        for (size_t t = a; t < b; ++t) marshal(t);
+      });
+      ph[0] = pc.lap("txset: marshal");
     }
     if (prefetched_pairs) *prefetched_pairs = pre.pairs();
     auto check = [&](size_t a, size_t b) {

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Developer tool: the host phases of config 3 (svh_check_txset with the batch
+pre-pass) on any machine.  Tx sets signed with libsodium; without a GPU the
+pre-pass's engine call fails over to the engine's CPU path, so only the
+marshal and pair-enumeration phases are meaningful there.  Prints the phase
+medians (ms) over `reps` runs of each of `sets` sets.
+
+  python tools/txset_host_probe.py [n_tx] [sets] [reps]"""
+import ctypes
+import importlib
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import txset_gen as tg  # noqa: E402
+
+SODIUM = "/opt/conda/lib/libsodium.so.23"
+
+
+def main():
+    n_tx = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
+    sets = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    sv = importlib.import_module("stellar-core_amd")
+    so = ctypes.CDLL(SODIUM)
+    assert so.sodium_init() >= 0
+
+    def sign(reqs):
+        out = []
+        for seed, msg in reqs:
+            pk, sk, s = (ctypes.create_string_buffer(k) for k in (32, 64, 64))
+            so.crypto_sign_seed_keypair(pk, sk, seed)
+            so.crypto_sign_detached(s, None, msg, ctypes.c_ulonglong(len(msg)), sk)
+            out.append((pk.raw, s.raw))
+        return out
+
+    host = ctypes.CDLL(sv.HOSTLIB_PATH)
+    host.svh_last_error_string.restype = ctypes.c_char_p
+    fast = os.environ.get("TXSET_PROBE_ENGINE") != "real"
+    if fast:
+        # the engine phase replaced by an accept-all stub (host phases only:
+        # without a GPU the engine's CPU path would take ~0.35 s per set)
+        VF = ctypes.CFUNCTYPE(ctypes.c_int, *([ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p]))
+        KF = ctypes.CFUNCTYPE(ctypes.c_int, *([ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p,
+                                                                        ctypes.c_void_p]))
+
+        def accept(pk, sig, msg, off, ln, n, verdict):
+            ctypes.memset(verdict, 1, n)
+            return 0
+
+        def accept_keyed(pk, sig, msg, off, ln, n, verdict, keys):
+            ctypes.memset(verdict, 1, n)
+            return 0
+        vf, kf = VF(accept), KF(accept_keyed)
+        host.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+        host.svh_set_test_keyed_verifier.argtypes = [ctypes.c_void_p]
+        host.svh_set_test_verifier(ctypes.cast(vf, ctypes.c_void_p))
+        host.svh_set_test_keyed_verifier(ctypes.cast(kf, ctypes.c_void_p))
+    rows = []
+    for k in range(sets):
+        txs = tg.generate(n_tx, sign, seed=4040 + k)
+        T, S, G = tg.to_ctypes(txs)
+        for _ in range(reps):
+            ok = np.zeros(n_tx, np.uint8)
+            used = np.zeros(n_tx, np.uint8)
+            pairs = ctypes.c_uint64()
+            host.svh_cache_clear()
+            rc = host.svh_check_txset(T, ctypes.c_size_t(n_tx), S, G, 1, ok.ctypes.data_as(ctypes.c_void_p),
+                                      used.ctypes.data_as(ctypes.c_void_p), ctypes.byref(pairs))
+            assert rc == 0, host.svh_last_error_string()
+            ph = (ctypes.c_double * 4)()
+            host.svh_txset_last_phases(ph)
+            rows.append(list(ph))
+    ph = np.median(np.array(rows), axis=0)
+    print("marshal %.3f  pair_enumeration %.3f  engine %.3f  checkers %.3f ms  (pairs %d)" %
+          (ph[0], ph[1], ph[2], ph[3], pairs.value))
+
+
+if __name__ == "__main__":
+    main()
