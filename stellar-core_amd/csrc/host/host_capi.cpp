@@ -461,9 +461,13 @@ int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
     std::vector<Clk::time_point> tSub(n), tVer(n), tMain(n);
     std::vector<uint8_t> cbVerdict(n, 2);
     // the main thread's queue (Peer::recvMessage posted by the continuation)
+    // (as an event loop's post: the waiting thread is woken only when it
+    // sleeps; a busy one finds the new items on its next pass -- a wake-up
+    // per item costs each continuation a futex call)
     std::mutex qm;
     std::condition_variable qcv;
     std::vector<size_t> q;
+    bool mainWaiting = false;
     q.reserve(n);
     (void)PubKeyUtils::flushEngineCounts();  // (the run's own counts are read at the end)
     std::vector<uint8_t> out(n, 2);
@@ -484,7 +488,11 @@ int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
         while (doneN < n) {
           {
             std::unique_lock<std::mutex> lk(qm);
-            qcv.wait(lk, [&] { return q.size() > head; });
+            while (q.size() <= head) {
+              mainWaiting = true;
+              qcv.wait(lk);
+            }
+            mainWaiting = false;
             local.assign(q.begin() + (ptrdiff_t)head, q.end());
             head = q.size();
           }
@@ -517,11 +525,13 @@ int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
               mb.submit(k, ByteSlice(sig + 64 * i, 64), ByteSlice(msg + msg_off[i], msg_len[i]), [&, i](bool v) {
                 tVer[i] = Clk::now();
                 cbVerdict[i] = v ? 1 : 0;
+                bool wake;
                 {
                   std::lock_guard<std::mutex> g(qm);
                   q.push_back(i);
+                  wake = mainWaiting;
                 }
-                qcv.notify_one();
+                if (wake) qcv.notify_one();
               });
             }
           }

@@ -190,18 +190,34 @@ struct Stage {
 // whose keys are all cached runs sv_comb_kernel, any other batch the octet
 // kernel, after which its new keys are queued for a table build on the
 // low-priority build stream.
-struct LatLane {
-  std::mutex mu;
-  bool ready = false;
-  hipStream_t stream = nullptr;  // verify work (highest priority)
-  hipStream_t build = nullptr;   // key-table builds (lowest priority)
-  hipStream_t hstream = nullptr; // a keyed batch's cache keys, beside the verify kernel (highest priority)
-  hipEvent_t ev_lat = nullptr, done = nullptr, keys_down = nullptr;
-  HostBuf h_in, h_out, h_build;
+// One latency batch in flight on the lane: its staging and streams.  The
+// lane's mutex covers a batch's planning and launch; its wait and copy-out
+// run outside it, so with two contexts the next batch (an SCP burst's second
+// micro-batch) is planned and launched while the first one runs, instead of
+// queueing behind it on the host (SV_LAT_CONTEXTS, default 2; 1 serialises).
+struct LatCtx {
+  hipStream_t stream = nullptr;   // verify work (highest priority)
+  hipStream_t hstream = nullptr;  // a keyed batch's cache keys, beside the verify kernel (highest priority)
+  hipEvent_t done = nullptr, keys_down = nullptr;
+  hipEvent_t ev = nullptr;        // (a key-table build waits for the work queued here)
+  HostBuf h_in, h_out;
   HostBuf z_out;   // mapped: the kernels write verdicts in place
   HostBuf z_keys;  // mapped: the hash kernel writes cache keys in place (keyed batches)
-  DevBuf d_in, d_out, d_keys, d_build;
+  DevBuf d_in, d_out, d_keys;
   DevBuf ws;  // the quad kernel's tables (cold batches above kOctetMax)
+  bool busy = false;  // (under LatLane::mu) a batch holds it
+};
+constexpr int kLatCtxMax = 2;
+struct LatLane {
+  std::mutex mu;
+  std::condition_variable freed;  // a context was released
+  bool ready = false;
+  int nctx = 1;
+  LatCtx ctx[kLatCtxMax];
+  hipStream_t build = nullptr;   // key-table builds (lowest priority)
+  hipEvent_t ev_lat = nullptr;   // (device-API batches: the caller's stream)
+  HostBuf h_build;
+  DevBuf d_build;
   void* ctab = nullptr;  // tables of B (built at lane init)
   DevBuf ktab, kstat;    // tables of -A per cached key, status per slot
   size_t cap = 0;        // key-cache capacity the index / tables are sized for
@@ -1147,11 +1163,26 @@ void lat_drop_builds(LatLane& L) {
 }
 
 // Caller holds L.mu and has set the device.
+// A context's quad workspace of at least `bytes`; growing it frees the old
+// one, so the work queued on the context (a device-API batch) drains first.
+int lat_ws(LatCtx& c, size_t bytes) {
+  if (bytes > c.ws.cap) (void)hipStreamSynchronize(c.stream);
+  return c.ws.ensure(bytes);
+}
+
+// Every batch queued on the lane's verify streams has completed.
+void lat_sync(LatLane& L) {
+  for (int k = 0; k < L.nctx; ++k) {
+    if (L.ctx[k].stream) (void)hipStreamSynchronize(L.ctx[k].stream);
+    if (L.ctx[k].hstream) (void)hipStreamSynchronize(L.ctx[k].hstream);
+  }
+}
+
+// (no batch holds a context: the API's teardown guard has drained the calls)
 void release_lat(LatLane& L) {
   if (!L.ready) return;
-  (void)hipStreamSynchronize(L.stream);
+  lat_sync(L);
   (void)hipStreamSynchronize(L.build);
-  if (L.hstream) (void)hipStreamSynchronize(L.hstream);
   lat_drop_builds(L);
   for (auto& pr : L.pending) {
     (void)hipEventDestroy(pr.first);
@@ -1159,22 +1190,27 @@ void release_lat(LatLane& L) {
   }
   L.pending.clear();
   L.pending_n.clear();
-  L.h_in.release(); L.h_out.release(); L.h_build.release();
-  L.z_out.release();
-  L.z_keys.release();
-  L.d_in.release(); L.d_out.release(); L.d_keys.release(); L.d_build.release();
-  L.ws.release();
+  for (LatCtx& c : L.ctx) {
+    c.h_in.release(); c.h_out.release(); c.z_out.release(); c.z_keys.release();
+    c.d_in.release(); c.d_out.release(); c.d_keys.release(); c.ws.release();
+    if (c.done) (void)hipEventDestroy(c.done);
+    if (c.keys_down) (void)hipEventDestroy(c.keys_down);
+    if (c.ev) (void)hipEventDestroy(c.ev);
+    if (c.stream) (void)hipStreamDestroy(c.stream);
+    if (c.hstream) (void)hipStreamDestroy(c.hstream);
+    c.done = c.keys_down = c.ev = nullptr;
+    c.stream = c.hstream = nullptr;
+    c.busy = false;
+  }
+  L.h_build.release();
+  L.d_build.release();
   L.ktab.release(); L.kstat.release();
   if (L.ctab) (void)hipFree(L.ctab);
   L.ctab = nullptr;
   if (L.ev_lat) (void)hipEventDestroy(L.ev_lat);
-  if (L.done) (void)hipEventDestroy(L.done);
-  if (L.keys_down) (void)hipEventDestroy(L.keys_down);
-  L.ev_lat = L.done = L.keys_down = nullptr;
-  if (L.stream) (void)hipStreamDestroy(L.stream);
+  L.ev_lat = nullptr;
   if (L.build) (void)hipStreamDestroy(L.build);
-  if (L.hstream) (void)hipStreamDestroy(L.hstream);
-  L.stream = L.build = L.hstream = nullptr;
+  L.build = nullptr;
   L.index.reset(0);
   L.cap = 0;
   L.ready = false;
@@ -1193,19 +1229,24 @@ int lat_ready(Device& D) {
   }
   int least = 0, greatest = 0;
   SV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-  SV_HIP(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, greatest));
-  L.z_out.mapped = true;
-  L.z_keys.mapped = true;
-  L.h_in.mapped = true;  // (the kernels read it in place: lat_in_place)
+  L.nctx = (int)std::min<size_t>(kLatCtxMax, std::max<size_t>(1, env_size("SV_LAT_CONTEXTS", 2)));
   L.ready = true;  // (release_lat cleans up whatever exists from here on)
-  hipError_t e = hipStreamCreateWithPriority(&L.build, hipStreamNonBlocking, least);
-  if (e == hipSuccess) e = hipStreamCreateWithPriority(&L.hstream, hipStreamNonBlocking, greatest);
+  hipError_t e = hipSuccess;
+  for (int k = 0; k < L.nctx && e == hipSuccess; ++k) {
+    LatCtx& c = L.ctx[k];
+    c.z_out.mapped = c.z_keys.mapped = true;
+    c.h_in.mapped = true;  // (the kernels read it in place: lat_in_place)
+    e = hipStreamCreateWithPriority(&c.stream, hipStreamNonBlocking, greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c.hstream, hipStreamNonBlocking, greatest);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c.done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c.keys_down, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c.ev, hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&L.build, hipStreamNonBlocking, least);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&L.ev_lat, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&L.done, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&L.keys_down, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc(&L.ctab, sv_comb_btab_bytes());
-  if (e == hipSuccess) e = sv_launch_comb_btab((uint32_t*)L.ctab, L.stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(L.stream);
+  if (e == hipSuccess) e = sv_launch_comb_btab((uint32_t*)L.ctab, L.ctx[0].stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(L.ctx[0].stream);
   if (e != hipSuccess) {
     release_lat(L);
     return hip_fail(e, "latency lane init");
@@ -1223,7 +1264,7 @@ int lat_ready(Device& D) {
 void lat_cache_ready(LatLane& L) {
   const size_t cap = key_cache_cap();
   if (cap == L.cap) return;
-  (void)hipStreamSynchronize(L.stream);
+  lat_sync(L);  // (no queued kernel reads the tables; a batch past its launch only copies out)
   (void)hipStreamSynchronize(L.build);
   lat_drop_builds(L);
   L.ktab.release();
@@ -1258,18 +1299,18 @@ void lat_poll(LatLane& L) {
 
 // Brackets the next launch on the lane's stream with timing events
 // (sv_timing_enable); lat_timing_end after the launch.
-int lat_timing_begin(LatLane& L, hipEvent_t* e0) {
+int lat_timing_begin(hipStream_t st, hipEvent_t* e0) {
   *e0 = nullptr;
   if (!g_timing.load()) return SV_OK;
   SV_HIP(hipEventCreate(e0));
-  SV_HIP(hipEventRecord(*e0, L.stream));
+  SV_HIP(hipEventRecord(*e0, st));
   return SV_OK;
 }
-int lat_timing_end(LatLane& L, hipEvent_t e0, uint64_t n) {
+int lat_timing_end(LatLane& L, hipStream_t st, hipEvent_t e0, uint64_t n) {
   if (!e0) return SV_OK;
   hipEvent_t e1 = nullptr;
   SV_HIP(hipEventCreate(&e1));
-  SV_HIP(hipEventRecord(e1, L.stream));
+  SV_HIP(hipEventRecord(e1, st));
   L.pending.emplace_back(e0, e1);
   L.pending_n.push_back(n);
   return SV_OK;
@@ -1327,8 +1368,9 @@ bool lat_plan(LatLane& L, const HostIn& in, size_t n) {
 }
 
 // Queues the table build of the keys lat_plan admitted, after everything
-// already on the lane's stream (a build may overwrite an evicted slot that an
-// earlier comb kernel reads).  A failed build only leaves its keys uncached.
+// already on the lane's verify streams (a build may overwrite an evicted slot
+// that an earlier comb kernel reads, on either context).  A failed build only
+// leaves its keys uncached.
 void lat_build(LatLane& L) {
   const size_t k = L.fresh_pk.size();
   if (!k) return;
@@ -1350,8 +1392,10 @@ void lat_build(LatLane& L) {
     e = hipEventCreateWithFlags(&b.uploaded, hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventRecord(L.ev_lat, L.stream);
-  if (e == hipSuccess) e = hipStreamWaitEvent(L.build, L.ev_lat, 0);
+  for (int c = 0; c < L.nctx && e == hipSuccess; ++c) {
+    e = hipEventRecord(L.ctx[c].ev, L.ctx[c].stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(L.build, L.ctx[c].ev, 0);
+  }
   if (e == hipSuccess) e = hipMemcpyAsync(L.d_build.p, h, 36 * k, hipMemcpyHostToDevice, L.build);
   if (e == hipSuccess) e = hipEventRecord(b.uploaded, L.build);
   if (e == hipSuccess)
@@ -1411,21 +1455,33 @@ bool lat_trace() {
 // Host-side stages of this thread's last latency-lane batch (sv_lat_last_trace).
 thread_local std::array<double, 8> t_lat_last{};
 
-// One latency-bound host batch on the slot's latency lane: pinned image (+
-// the key slots when warm) read in place (or one H2D), [hash kernel, keys D2H], the comb kernel
-// (every key cached) or the octet kernel, one D2H, one sync.
-int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, const KeysCb& kcb,
-                     bool* cb_done) {
+// What a launched latency batch leaves for its completion (lat_finish).
+struct LatPending {
+  size_t n = 0;
+  bool warm = false, early = false, zc = false, zk = false, in_place = false;
+  const uint8_t* vho = nullptr;  // its verdicts on the host, once `done`
+  uint8_t* kho = nullptr;        // its cache keys on the host, once `keys_down`
+  std::chrono::steady_clock::time_point t0, t1, t_up, t_k, t_down, t_b;
+};
+
+// One latency-bound host batch on context c of the slot's latency lane,
+// launched (caller holds L.mu): pinned image (+ the key slots when warm) read
+// in place (or one H2D), [hash kernel, keys D2H], the comb kernel (every key
+// cached) or the octet / quad kernel, one D2H; then the key-table builds it
+// admitted.  lat_finish waits and copies out, without the lock.
+int lat_launch_locked(Device& D, LatCtx& c, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys,
+                      const KeysCb& kcb, LatPending& pd) {
   LatLane& L = D.lat;
   int rc;
-  if ((rc = lat_ready(D))) return rc;
-  const auto t0 = std::chrono::steady_clock::now();
+  pd.t0 = std::chrono::steady_clock::now();
+  pd.n = n;
   D.lat_last_ns.store(now_ns(), std::memory_order_relaxed);
   lat_cache_ready(L);
   lat_poll(L);
   const uint32_t dbg = g_dbg.load() & kKernelDbgMask;
   // (the lattice test knobs select the octet kernel's code paths)
   const bool warm = lat_plan(L, in, n) && verdict && dbg == 0;
+  pd.warm = warm;
   size_t msg_total;
   const Image im = image_of(in, 0, n, &msg_total);
   const size_t o_ks = (im.bytes + 3) & ~(size_t)3;
@@ -1434,104 +1490,144 @@ int lat_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, ui
   // the kernels straight into mapped pinned memory, no D2H blit
   const bool zc = verdict && lat_zero_copy();
   const bool zk = keys && lat_zero_copy();
+  pd.zc = zc;
+  pd.zk = zk;
   const size_t out_per = (verdict && !zc ? 1 : 0) + (keys && !zk ? 32 : 0);
   const bool in_place = lat_in_place();
-  if ((rc = L.h_in.ensure(in_bytes)) || (!in_place && (rc = L.d_in.ensure(in_bytes)))) return rc;
-  if (zc && (rc = L.z_out.ensure(n))) return rc;
-  if (zk && (rc = L.z_keys.ensure(32 * n))) return rc;
-  if (out_per && (rc = L.h_out.ensure(out_per * n))) return rc;
-  if (verdict && !zc && (rc = L.d_out.ensure(n))) return rc;
-  if (keys && !zk && (rc = L.d_keys.ensure(32 * n))) return rc;
-  uint8_t* h = (uint8_t*)L.h_in.p;
+  pd.in_place = in_place;
+  if ((rc = c.h_in.ensure(in_bytes)) || (!in_place && (rc = c.d_in.ensure(in_bytes)))) return rc;
+  if (zc && (rc = c.z_out.ensure(n))) return rc;
+  if (zk && (rc = c.z_keys.ensure(32 * n))) return rc;
+  if (out_per && (rc = c.h_out.ensure(out_per * n))) return rc;
+  if (verdict && !zc && (rc = c.d_out.ensure(n))) return rc;
+  if (keys && !zk && (rc = c.d_keys.ensure(32 * n))) return rc;
+  uint8_t* h = (uint8_t*)c.h_in.p;
   pack(in, 0, n, im, h);
   if (warm) std::memcpy(h + o_ks, L.kslots.data(), 4 * n);
-  const auto t1 = std::chrono::steady_clock::now();
-  if (!in_place) SV_HIP(hipMemcpyAsync(L.d_in.p, h, in_bytes, hipMemcpyHostToDevice, L.stream));
-  const auto t_up = std::chrono::steady_clock::now();
-  uint8_t* d = (uint8_t*)(in_place ? L.h_in.dp : L.d_in.p);
-  void* d_verdict = zc ? L.z_out.dp : L.d_out.p;
-  void* d_keys = zk ? L.z_keys.dp : L.d_keys.p;
+  pd.t1 = std::chrono::steady_clock::now();
+  if (!in_place) SV_HIP(hipMemcpyAsync(c.d_in.p, h, in_bytes, hipMemcpyHostToDevice, c.stream));
+  pd.t_up = std::chrono::steady_clock::now();
+  uint8_t* d = (uint8_t*)(in_place ? c.h_in.dp : c.d_in.p);
+  void* d_verdict = zc ? c.z_out.dp : c.d_out.p;
+  void* d_keys = zk ? c.z_keys.dp : c.d_keys.p;
   const uint64_t* d_off = im.var ? (const uint64_t*)(d + im.o_off) : nullptr;
   const uint32_t* d_len = im.var ? (const uint32_t*)(d + im.o_len) : nullptr;
-  uint8_t* ho = (uint8_t*)L.h_out.p;
-  const uint8_t* vho = zc ? (const uint8_t*)L.z_out.p : ho;  // verdicts on the host
-  uint8_t* kho = zk ? (uint8_t*)L.z_keys.p : ho + (verdict && !zc ? n : 0);  // keys on the host
-  const bool early = kcb && keys && verdict;
-  auto t_k = t_up;
-  // A keyed batch's cache keys: with the image read in place, on the lane's
-  // second stream, beside the verify kernel (the caller's cache walk then
-  // overlaps the verification); the windows are staged in LDS (kind 2).
+  uint8_t* ho = (uint8_t*)c.h_out.p;
+  pd.vho = zc ? (const uint8_t*)c.z_out.p : ho;                  // verdicts on the host
+  pd.kho = zk ? (uint8_t*)c.z_keys.p : ho + (verdict && !zc ? n : 0);  // keys on the host
+  pd.early = kcb && keys && verdict;
+  pd.t_k = pd.t_up;
+  // A keyed batch's cache keys: with the image read in place, on the
+  // context's second stream, beside the verify kernel (the caller's cache
+  // walk then overlaps the verification); the windows are staged in LDS (kind 2).
   const bool kside = keys && in_place;
-  hipStream_t ks = kside ? L.hstream : L.stream;
+  hipStream_t ks = kside ? c.hstream : c.stream;
   if (keys) {
     SV_HIP(sv_launch_hash(in_place ? 2 : 0, D.grid * 2, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
                           d_keys, ks));
-    if (!zk) SV_HIP(hipMemcpyAsync(kho, L.d_keys.p, 32 * n, hipMemcpyDeviceToHost, ks));
-    SV_HIP(hipEventRecord(L.keys_down, ks));
+    if (!zk) SV_HIP(hipMemcpyAsync(pd.kho, c.d_keys.p, 32 * n, hipMemcpyDeviceToHost, ks));
+    SV_HIP(hipEventRecord(c.keys_down, ks));
   }
   if (verdict) {
     const int mode = im.var ? 1 : (in.fixed == 32 ? 0 : 2);
     hipEvent_t e0;
-    if ((rc = lat_timing_begin(L, &e0))) return rc;
+    if ((rc = lat_timing_begin(c.stream, &e0))) return rc;
     // (while bulk work runs, only the 1-signature-per-wave geometry fits the
     // slot a shared-mode bulk launch leaves free on each CU)
     const bool bulk_busy = hipStreamQuery(D.stream) == hipErrorNotReady;
     if (warm)
       SV_HIP(sv_launch_comb(mode, bulk_busy ? 1 : sv_comb_spw(n, D.cus), d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
                             d_verdict, (const uint32_t*)(d + o_ks), (const uint32_t*)L.ktab.p,
-                            (const uint32_t*)L.kstat.p, (const uint32_t*)L.ctab, L.stream));
+                            (const uint32_t*)L.kstat.p, (const uint32_t*)L.ctab, c.stream));
     else if (n > kOctetMax && !(g_dbg.load() & SV_DBG_NO_QUAD)) {
-      if ((rc = L.ws.ensure(sv_verify_ws_bytes(kGeomQuad, 0, n)))) return rc;
+      if ((rc = lat_ws(c, sv_verify_ws_bytes(kGeomQuad, 0, n)))) return rc;
       SV_HIP(sv_launch_verify(mode, kGeomQuad, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n, d_verdict,
-                              nullptr, L.ws.p, D.btab, dbg | SV_KP_LAT, 0, nullptr, L.stream));
+                              nullptr, c.ws.p, D.btab, dbg | SV_KP_LAT, 0, nullptr, c.stream));
     } else
       SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
-                              d_verdict, nullptr, nullptr, D.btab, dbg, 0, nullptr, L.stream));
-    if ((rc = lat_timing_end(L, e0, n))) return rc;
-    t_k = std::chrono::steady_clock::now();
-    if (!zc) SV_HIP(hipMemcpyAsync(ho, L.d_out.p, n, hipMemcpyDeviceToHost, L.stream));
+                              d_verdict, nullptr, nullptr, D.btab, dbg, 0, nullptr, c.stream));
+    if ((rc = lat_timing_end(L, c.stream, e0, n))) return rc;
+    pd.t_k = std::chrono::steady_clock::now();
+    if (!zc) SV_HIP(hipMemcpyAsync(ho, c.d_out.p, n, hipMemcpyDeviceToHost, c.stream));
   }
-  SV_HIP(hipEventRecord(L.done, L.stream));
-  const auto t_down = std::chrono::steady_clock::now();
-  if (early) {
-    SV_HIP(hipEventSynchronize(L.keys_down));
-    std::memcpy(keys, kho, 32 * n);
+  SV_HIP(hipEventRecord(c.done, c.stream));
+  pd.t_down = std::chrono::steady_clock::now();
+  lat_build(L);  // (after the verify work: a build waits for it on the device)
+  pd.t_b = std::chrono::steady_clock::now();
+  if (warm) ++L.warm;
+  else ++L.cold;
+  return SV_OK;
+}
+
+// The rest of a launched batch, without the lane's lock: the keys-ready
+// callback, the wait, the copy-out.
+int lat_finish(LatCtx& c, const LatPending& pd, uint8_t* verdict, uint8_t* keys, const KeysCb& kcb, bool* cb_done) {
+  const size_t n = pd.n;
+  if (pd.early) {
+    SV_HIP(hipEventSynchronize(c.keys_down));
+    std::memcpy(keys, pd.kho, 32 * n);
     kcb(n);
     *cb_done = true;
   }
-  lat_build(L);  // (after the verify work: a build waits for it on the device)
-  const auto t_b = std::chrono::steady_clock::now();
-  SV_HIP(hipEventSynchronize(L.done));
-  if (keys && !early) SV_HIP(hipEventSynchronize(L.keys_down));
-  if (verdict) std::memcpy(verdict, vho, n);
-  if (keys && !early) std::memcpy(keys, kho, 32 * n);
-  if (warm) ++L.warm;
-  else ++L.cold;
+  SV_HIP(hipEventSynchronize(c.done));
+  if (keys && !pd.early) SV_HIP(hipEventSynchronize(c.keys_down));
+  if (verdict) std::memcpy(verdict, pd.vho, n);
+  if (keys && !pd.early) std::memcpy(keys, pd.kho, 32 * n);
   const auto t2 = std::chrono::steady_clock::now();
   auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
     return std::chrono::duration<double, std::micro>(b - a).count();
   };
-  t_lat_last = {us(t0, t1), us(t1, t_up), us(t_up, t_k), us(t_k, t_down), us(t_down, t_b), us(t_b, t2), us(t0, t2),
-                warm ? 1.0 : 0.0};
+  t_lat_last = {us(pd.t0, pd.t1), us(pd.t1, pd.t_up), us(pd.t_up, pd.t_k), us(pd.t_k, pd.t_down),
+                us(pd.t_down, pd.t_b), us(pd.t_b, t2), us(pd.t0, t2), pd.warm ? 1.0 : 0.0};
   if (lat_trace()) {
     fprintf(stderr,
             "SV_LAT_TRACE n=%zu %s plan+pack %.1f us | h2d call %.1f launch %.1f d2h+rec %.1f build %.1f sync %.1f"
             " | device %.1f us @%.1f%s\n",
-            n, warm ? "warm" : "cold", us(t0, t1), us(t1, t_up), us(t_up, t_k), us(t_k, t_down), us(t_down, t_b),
-            us(t_b, t2), us(t1, t2), trace_abs_us() - us(t0, t2), in_place ? " in place" : "");
+            n, pd.warm ? "warm" : "cold", us(pd.t0, pd.t1), us(pd.t1, pd.t_up), us(pd.t_up, pd.t_k),
+            us(pd.t_k, pd.t_down), us(pd.t_down, pd.t_b), us(pd.t_b, t2), us(pd.t1, t2),
+            trace_abs_us() - us(pd.t0, t2), pd.in_place ? " in place" : "");
   }
   return SV_OK;
 }
 
 int lat_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* keys, const KeysCb& kcb,
               bool* cb_done) {
-  std::lock_guard<std::mutex> g(D.lat.mu);
+  LatLane& L = D.lat;
+  std::unique_lock<std::mutex> lk(L.mu);
   SV_HIP(hipSetDevice(D.phys));
-  const int rc = lat_slice_locked(D, in, n, verdict, keys, kcb, cb_done);
-  if (rc != SV_OK && D.lat.ready) {  // nothing of this call in flight
-    (void)hipStreamSynchronize(D.lat.stream);
-    if (D.lat.hstream) (void)hipStreamSynchronize(D.lat.hstream);
+  int rc;
+  if ((rc = lat_ready(D))) return rc;
+  // a free context (every one busy: wait for the first batch to finish)
+  LatCtx* c = nullptr;
+  L.freed.wait(lk, [&] {
+    for (int k = 0; k < L.nctx; ++k)
+      if (!L.ctx[k].busy) {
+        c = &L.ctx[k];
+        return true;
+      }
+    return false;
+  });
+  c->busy = true;
+  auto release = [&] {
+    c->busy = false;
+    L.freed.notify_one();
+  };
+  LatPending pd;
+  rc = lat_launch_locked(D, *c, in, n, verdict, keys, kcb, pd);
+  if (rc != SV_OK) {  // nothing of this call in flight
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->hstream);
+    release();
+    return rc;
   }
+  lk.unlock();
+  rc = lat_finish(*c, pd, verdict, keys, kcb, cb_done);
+  if (rc != SV_OK) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->hstream);
+  }
+  lk.lock();
+  release();
   return rc;
 }
 
@@ -2001,23 +2097,34 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
     // the latency lane (octet kernel: the keys are in device memory, so the
     // host-side key cache is not consulted)
     LatLane& L = D.lat;
-    std::lock_guard<std::mutex> g(L.mu);
+    std::unique_lock<std::mutex> lk(L.mu);
     SV_HIP(hipSetDevice(D.phys));
     if ((rc = lat_ready(D))) return rc;
+    // a context no host batch holds (this call only queues work: it leaves
+    // the context free, and a later batch on it runs after this one)
+    LatCtx* c = nullptr;
+    L.freed.wait(lk, [&] {
+      for (int k = 0; k < L.nctx; ++k)
+        if (!L.ctx[k].busy) {
+          c = &L.ctx[k];
+          return true;
+        }
+      return false;
+    });
     D.lat_last_ns.store(now_ns(), std::memory_order_relaxed);
     SV_HIP(hipEventRecord(L.ev_lat, user));
-    SV_HIP(hipStreamWaitEvent(L.stream, L.ev_lat, 0));
+    SV_HIP(hipStreamWaitEvent(c->stream, L.ev_lat, 0));
     hipEvent_t e0;
     const uint32_t dbg = g_dbg.load() & kKernelDbgMask;
     const bool quad = n > kOctetMax && !(g_dbg.load() & SV_DBG_NO_QUAD);
-    if (quad && (rc = L.ws.ensure(sv_verify_ws_bytes(kGeomQuad, 0, n)))) return rc;
-    if ((rc = lat_timing_begin(L, &e0))) return rc;
+    if (quad && (rc = lat_ws(*c, sv_verify_ws_bytes(kGeomQuad, 0, n)))) return rc;
+    if ((rc = lat_timing_begin(c->stream, &e0))) return rc;
     SV_HIP(sv_launch_verify(mode, quad ? kGeomQuad : SV_PATH_LATENCY, 1, d_pk, d_sig, d_msg, d_msg_off, d_msg_len,
-                            fixed_msg_len, n, d_verdict, d_bitmap, quad ? L.ws.p : nullptr, D.btab,
-                            quad ? (dbg | SV_KP_LAT) : dbg, 0, nullptr, L.stream));
-    if ((rc = lat_timing_end(L, e0, n))) return rc;
-    SV_HIP(hipEventRecord(L.done, L.stream));
-    SV_HIP(hipStreamWaitEvent(user, L.done, 0));
+                            fixed_msg_len, n, d_verdict, d_bitmap, quad ? c->ws.p : nullptr, D.btab,
+                            quad ? (dbg | SV_KP_LAT) : dbg, 0, nullptr, c->stream));
+    if ((rc = lat_timing_end(L, c->stream, e0, n))) return rc;
+    SV_HIP(hipEventRecord(c->done, c->stream));
+    SV_HIP(hipStreamWaitEvent(user, c->done, 0));
     return SV_OK;
   }
   std::lock_guard<std::mutex> g(D.mu);
@@ -2152,7 +2259,7 @@ int sv_device_synchronize(int device) {
   if (!D.ready) return SV_OK;
   SV_HIP(hipSetDevice(D.phys));
   SV_HIP(hipStreamSynchronize(D.stream));
-  if (D.lat.ready) SV_HIP(hipStreamSynchronize(D.lat.stream));
+  if (D.lat.ready) lat_sync(D.lat);
   return SV_OK;
 }
 
@@ -2243,7 +2350,7 @@ int sv_pinned_bytes(int device, size_t* bytes) {
   std::lock_guard<std::mutex> g(Dp->mu);
   size_t b = 0;
   for (Stage& s : Dp->st) b += s.h_in.cap + s.h_out.cap;
-  b += Dp->z_in.cap;
+  b += Dp->z_in.cap + Dp->z_out.cap;
   *bytes = b;
   return SV_OK;
 }

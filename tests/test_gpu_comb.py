@@ -11,6 +11,8 @@ keys for a table build.  Both must give libsodium's verdict on every row:
     at sizes that select each kernel geometry (1, 2 and 4 signatures per
     chain wave), against the oracle;
   * eviction: a cache smaller than the key set still gives exact verdicts;
+  * batches from several threads at once (two run side by side on the lane),
+    with eviction churn and warm;
   * the staged-copy lane (SV_LAT_ZC_IN=0 / SV_LAT_ZERO_COPY=0: one H2D of the
     image, one D2H of the verdicts) gives the same verdicts as the default
     (kernels read the image and write the verdicts in mapped memory);
@@ -162,6 +164,42 @@ def test_small_cache_evicts_exactly(sv, gpu, oracle):
         st = sv.key_cache_stats(0)
         assert st["capacity"] == 64 and st["keys"] <= 64
         assert st["evictions"] > 0
+    finally:
+        sv.set_key_cache(1024)
+
+
+@pytest.mark.parametrize("cap", [64, 8192])
+def test_concurrent_lane_batches(sv, gpu, oracle, cap):
+    """Batches from several host threads at once: the lane plans and launches
+    them one at a time but runs up to two side by side (sv_api.cpp LatCtx).
+    With a 64-key cache under a 600-key workload every batch evicts and queues
+    table builds while the other context's comb kernel reads the tables; with a
+    large one the same sets run warm side by side.  Every verdict exact."""
+    import threading
+    sets = [_scp_set(oracle, 200 + 37 * k, seed=2000 + k) for k in range(6)]
+    sv.set_key_cache(cap)
+    errors = []
+    try:
+        def worker(t):
+            try:
+                for it in range(10):
+                    d = sets[(t * 5 + it) % len(sets)]
+                    out = _run(sv, d)
+                    bad = np.nonzero(out != d["verdict"])[0]
+                    if len(bad):
+                        errors.append((t, it, bad[:5].tolist()))
+            except Exception as e:  # (reported below, not swallowed)
+                errors.append((t, repr(e)))
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errors, errors[:5]
+        st = sv.key_cache_stats(0)
+        assert st["warm_batches"] + st["cold_batches"] >= 40
+        if cap == 64:
+            assert st["evictions"] > 0
     finally:
         sv.set_key_cache(1024)
 
