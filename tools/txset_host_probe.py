@@ -10,6 +10,7 @@ import ctypes
 import importlib
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -69,15 +70,17 @@ def main():
             used = np.zeros(n_tx, np.uint8)
             pairs = ctypes.c_uint64()
             host.svh_cache_clear()
+            t_call = time.perf_counter()
             rc = host.svh_check_txset(T, ctypes.c_size_t(n_tx), S, G, 1, ok.ctypes.data_as(ctypes.c_void_p),
                                       used.ctypes.data_as(ctypes.c_void_p), ctypes.byref(pairs))
             assert rc == 0, host.svh_last_error_string()
+            t_call = (time.perf_counter() - t_call) * 1e3
             ph = (ctypes.c_double * 4)()
             host.svh_txset_last_phases(ph)
-            rows.append(list(ph))
+            rows.append(list(ph) + [t_call])
     ph = np.median(np.array(rows), axis=0)
-    print("marshal %.3f  pair_enumeration %.3f  engine %.3f  checkers %.3f ms  (pairs %d)" %
-          (ph[0], ph[1], ph[2], ph[3], pairs.value))
+    print("marshal %.3f  pair_enumeration %.3f  engine %.3f  checkers %.3f ms  call %.3f ms  (pairs %d)" %
+          (ph[0], ph[1], ph[2], ph[3], ph[4], pairs.value))
 
 
 if __name__ == "__main__":
