@@ -204,6 +204,62 @@ def test_concurrent_lane_batches(sv, gpu, oracle, cap):
         sv.set_key_cache(1024)
 
 
+def test_device_and_host_lane_batches_concurrent(sv, gpu, oracle):
+    """Device-API lane batches (queued on a free context, not waited for) from
+    one thread while host lane batches run on the contexts from two others:
+    stream order keeps each context's work apart, every verdict exact."""
+    import threading
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    n = 3000
+    rng = np.random.default_rng(77)
+    seeds = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).to(dev)
+    msgs = torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).to(dev)
+    pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    sv.sign_device(0, seeds.data_ptr(), msgs.data_ptr(), n, pk.data_ptr(), sig.data_ptr(), st)
+    torch.cuda.synchronize(dev)
+    sig[::5, 40] ^= 0x08
+    want_d = np.ones(n, np.uint8)
+    want_d[::5] = 0
+    sets = [_scp_set(oracle, 400 + 50 * k, seed=3000 + k) for k in range(3)]
+    errors = []
+
+    def device_worker():
+        try:
+            s = torch.cuda.Stream(dev)
+            out = torch.zeros(n, dtype=torch.uint8, device=dev)
+            for it in range(12):
+                with torch.cuda.stream(s):
+                    out.zero_()
+                    sv.verify_device(0, pk.data_ptr(), sig.data_ptr(), msgs.data_ptr(), n, out.data_ptr(), 0,
+                                     s.cuda_stream)
+                s.synchronize()
+                got = out.cpu().numpy()
+                if not np.array_equal(got, want_d):
+                    errors.append(("device", it, np.nonzero(got != want_d)[0][:5].tolist()))
+        except Exception as e:
+            errors.append(("device", repr(e)))
+
+    def host_worker(t):
+        try:
+            for it in range(10):
+                d = sets[(t + it) % len(sets)]
+                out = _run(sv, d)
+                if not (out == d["verdict"]).all():
+                    errors.append(("host", t, it))
+        except Exception as e:
+            errors.append(("host", t, repr(e)))
+
+    th = [threading.Thread(target=device_worker)] + [threading.Thread(target=host_worker, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]
+
+
 def test_cache_off_is_octet_only(sv, gpu, golden):
     sv.set_key_cache(0)
     try:
