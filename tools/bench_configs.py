@@ -308,8 +308,9 @@ def config3(env, n_tx=5000, sets=5):
     phase_split = {k: float(np.median(ph[:, j])) for j, k in enumerate(
         ("marshal_ms", "pair_enumeration_ms", "engine_prepass_ms", "checkers_ms"))}
     phase_split["per_set"] = [[round(float(x), 3) for x in row] for row in ph]
-    phase_split["what"] = ("svh_txset_last_phases medians over the distinct sets: C structs -> mirror objects, "
-                           "SignatureBatchPrefetch::addBatch (pair enumeration), run() (one GPU batch + side "
+    phase_split["what"] = ("svh_txset_last_phases medians over the distinct sets: marshal = the mirror objects' "
+                           "allocation (the C structs are marshalled per tx inside the pair-enumeration pass, "
+                           "SignatureBatchPrefetch::addBatch with its prepare hook), run() (one GPU batch + side "
                            "table), the checkers on the host pool")
     dt_rep = min(run(cts, 1)[2] for _ in range(3))  # the first set again (warm per-key state): not the headline
     out = {"txs": n_tx, "decorated_signatures": nsig, "prefetched_pairs": pairs, "generate_s": gen_s,
