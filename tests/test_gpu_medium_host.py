@@ -7,6 +7,8 @@ corruptions; golden fixture rows with libsodium's verdicts) at the sizes
 VERDICT r4 names (29,217 and 100k) and around the crossovers; consecutive
 calls reuse the in-place image and verdict buffers.
 """
+import hashlib
+
 import numpy as np
 import pytest
 
@@ -101,3 +103,49 @@ def test_medium_variable_length_fixture_rows(sv, dev, golden, geom):
         sv.set_key_tables(prev_kt)
     bad = np.nonzero(out != want)[0]
     assert len(bad) == 0, bad[:10]
+
+
+@pytest.mark.parametrize("n", [1000, 12289, 29217, 50000])
+def test_uniform_length_variable_batches(sv, dev, signed, n):
+    """A variable-length call whose messages all have one length goes to the
+    device as a fixed-length batch (sv_api.cpp uniform_form): messages found
+    by their offsets (here shuffled, and rows sharing one message as a tx's
+    pairs share its contents hash) and packed at a fixed stride."""
+    P, S, M = signed
+    p, s, m, want = _corrupt(P, S, M, n, 7000 + n)
+    rng = np.random.default_rng(n)
+    perm = rng.permutation(n)
+    buf = np.ascontiguousarray(m[perm]).reshape(-1)  # message of row i at slot inv[i]
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n)
+    off = (inv * 32).astype(np.uint64)
+    ln = np.full(n, 32, np.uint32)
+    out = sv.verify_batch(p, s, buf, off, ln, device=0)
+    assert np.array_equal(out, want), np.nonzero(out != want)[0][:10]
+    # keyed: the cache keys are over the same bytes
+    k = min(n, 2000)
+    v2, k2 = sv.verify_batch_keyed(p[:k], s[:k], buf, off[:k], ln[:k], device=0)
+    assert np.array_equal(v2, want[:k])
+    for i in range(0, k, 97):
+        o = int(off[i])
+        h = hashlib.blake2b(p[i].tobytes() + s[i].tobytes() + buf[o:o + 32].tobytes(), digest_size=32).digest()
+        assert k2[i].tobytes() == h, i
+
+
+def test_uniform_length_shared_and_other_lengths(sv, dev, golden):
+    """Rows sharing one message (one offset), and uniform lengths other than 32
+    (every fixture row of one length), against libsodium's verdicts."""
+    d = golden["msglen"]
+    for L in sorted(set(int(x) for x in d["msg_len"]))[1::37]:
+        rows = np.nonzero(d["msg_len"] == L)[0]
+        if len(rows) == 0:
+            continue
+        reps = max(1, 400 // len(rows))
+        r = np.tile(rows, reps)
+        out = sv.verify_batch(d["pk"][r], d["sig"][r], d["msg"], d["msg_off"][r], d["msg_len"][r], device=0)
+        assert np.array_equal(out, d["verdict"][r]), L
+    v = golden["valid"]
+    rows = np.nonzero(v["msg_len"] == 32)[0][:50]
+    r = np.repeat(rows, 40)  # each message shared by 40 rows
+    out = sv.verify_batch(v["pk"][r], v["sig"][r], v["msg"], v["msg_off"][r], v["msg_len"][r], device=0)
+    assert np.array_equal(out, v["verdict"][r])
