@@ -144,6 +144,15 @@ def test_uniform_length_shared_and_other_lengths(sv, dev, golden):
         r = np.tile(rows, reps)
         out = sv.verify_batch(d["pk"][r], d["sig"][r], d["msg"], d["msg_off"][r], d["msg_len"][r], device=0)
         assert np.array_equal(out, d["verdict"][r]), L
+    # long messages (513 B .. 64 KiB - 1, every class): one length at a time,
+    # the fixed path's read-from-memory branch on every kernel geometry
+    d = golden["longmsg"]
+    for L in sorted(set(int(x) for x in d["msg_len"])):
+        rows = np.nonzero(d["msg_len"] == L)[0]
+        for path in ("latency", "throughput"):
+            out = sv.verify_batch(d["pk"][rows], d["sig"][rows], d["msg"], d["msg_off"][rows], d["msg_len"][rows],
+                                  device=0, path=path)
+            assert np.array_equal(out, d["verdict"][rows]), (L, path)
     v = golden["valid"]
     rows = np.nonzero(v["msg_len"] == 32)[0][:50]
     r = np.repeat(rows, 40)  # each message shared by 40 rows
