@@ -1614,9 +1614,12 @@ int lat_slice(Device& D, const HostIn& in, size_t n, uint8_t* verdict, uint8_t* 
     return false;
   });
   c->busy = true;
+  // (notify_all: a device-API caller waiting here takes no context, so a
+  // single wake-up could land on it and leave a host batch asleep beside a
+  // free one)
   auto release = [&] {
     c->busy = false;
-    L.freed.notify_one();
+    L.freed.notify_all();
   };
   LatPending pd;
   rc = lat_launch_locked(D, *c, in, n, verdict, keys, kcb, pd);
