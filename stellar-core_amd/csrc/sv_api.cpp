@@ -2125,20 +2125,18 @@ int sv_ed25519_verify_device(int device, const void* d_pk, const void* d_sig, co
     // the latency lane (octet kernel: the keys are in device memory, so the
     // host-side key cache is not consulted)
     LatLane& L = D.lat;
-    std::unique_lock<std::mutex> lk(L.mu);
+    std::lock_guard<std::mutex> g(L.mu);
     SV_HIP(hipSetDevice(D.phys));
     if ((rc = lat_ready(D))) return rc;
-    // a context no host batch holds (this call only queues work: it leaves
-    // the context free, and a later batch on it runs after this one)
-    LatCtx* c = nullptr;
-    L.freed.wait(lk, [&] {
-      for (int k = 0; k < L.nctx; ++k)
-        if (!L.ctx[k].busy) {
-          c = &L.ctx[k];
-          return true;
-        }
-      return false;
-    });
+    // a context no host batch holds, else the first: this call only queues
+    // work (stream order keeps it after a batch running on the same context,
+    // and the workspace only grows once that context's stream has drained)
+    LatCtx* c = &L.ctx[0];
+    for (int k = 0; k < L.nctx; ++k)
+      if (!L.ctx[k].busy) {
+        c = &L.ctx[k];
+        break;
+      }
     D.lat_last_ns.store(now_ns(), std::memory_order_relaxed);
     SV_HIP(hipEventRecord(L.ev_lat, user));
     SV_HIP(hipStreamWaitEvent(c->stream, L.ev_lat, 0));
