@@ -1443,6 +1443,16 @@ bool lat_zero_copy() {
 // 0.112 / 0.253 / 0.508 ms, and a staged copy queues behind a bulk call's
 // chunk upload (up to ~0.8 ms per 32 MB chunk): p99 under the 2^22 host
 // batch 0.61-0.86 -> 0.22 ms (profiles/r04/isolation/).
+// Cold latency batches of at most this many signatures take the three-wave
+// octet kernel (SV_OCT_HI_MAX; 0: never).  Measured (profiles/r05/octet_hi/):
+// p50 1k 0.241-0.245 -> 0.221-0.226 ms, 2k 0.256 -> 0.240, 4k 0.378 -> 0.375;
+// at 6k the third wave's repeated doublings cost more than they save (0.50
+// against 0.42-0.44 ms).
+size_t oct_hi_max() {
+  static const size_t v = env_size("SV_OCT_HI_MAX", 4096);
+  return v;
+}
+
 bool lat_in_place() {
   static const bool b = env_size("SV_LAT_ZC_IN", 1) != 0;
   return b;
@@ -1549,9 +1559,14 @@ int lat_launch_locked(Device& D, LatCtx& c, const HostIn& in, size_t n, uint8_t*
       if ((rc = lat_ws(c, sv_verify_ws_bytes(kGeomQuad, 0, n)))) return rc;
       SV_HIP(sv_launch_verify(mode, kGeomQuad, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n, d_verdict,
                               nullptr, c.ws.p, D.btab, dbg | SV_KP_LAT, 0, nullptr, c.stream));
-    } else
+    } else {
+      // (a third wave per workgroup takes the chains' top windows while no
+      // bulk work runs: its larger workgroup would not fit the slot a
+      // shared-mode bulk launch leaves free)
+      const uint32_t hi = (!bulk_busy && n <= oct_hi_max()) ? SV_KP_OCT_HI : 0u;
       SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
-                              d_verdict, nullptr, nullptr, D.btab, dbg, 0, nullptr, c.stream));
+                              d_verdict, nullptr, nullptr, D.btab, dbg | hi, 0, nullptr, c.stream));
+    }
     if ((rc = lat_timing_end(L, c.stream, e0, n))) return rc;
     pd.t_k = std::chrono::steady_clock::now();
     if (!zc) SV_HIP(hipMemcpyAsync(ho, c.d_out.p, n, hipMemcpyDeviceToHost, c.stream));

@@ -503,6 +503,21 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
 // per half) while wave 0 runs the -A / -R chains without base additions;
 // wave 0 adds the result at the end (second LDS handoff).
 #define SV_OCTET_BLOCK 128
+// HI (cold batches while no bulk work runs, sv_launch_verify): a third wave
+// per workgroup runs the top windows of the -A / -R chains.  It waits for the
+// decoded points at the table barrier, doubles them 4 Wlo times (Q = 16^Wlo P),
+// builds Q's tables in LDS and runs windows W-1 .. Wlo; wave 0 runs Wlo-1 .. 0
+// and adds the high part at the second barrier.  The third wave repeats the
+// doublings, so what it saves is the additions of its windows: balanced at
+// about W / 9 of them.
+#define SV_OCTET_BLOCK_HI 192
+#ifndef SV_OCT_HI_DIV
+#define SV_OCT_HI_DIV 9
+#endif
+__device__ __forceinline__ int sv_oct_hi_windows(int W) {
+  const int h = (W + SV_OCT_HI_DIV / 2) / SV_OCT_HI_DIV;
+  return h < 1 ? 1 : (h > W ? W : h);
+}
 
 // The tables (23 KB) are dynamic LDS, placed after the static arrays below:
 // measured 2.2 us faster per cold 1k batch than the same tables as the first
@@ -512,13 +527,37 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
 // MSG: launches of at most one workgroup per CU (n <= 8 per CU) only; larger
 // ones read the message from memory (the extra 4 KB would cost a
 // workgroup slot per CU: 12288 cold 0.58 -> 0.80 ms).
-#define SV_OCTET_LDS_BYTES(MSG) (SV_OCTET_TAB_BYTES + ((MSG) ? SV_OSIGS * SV_MSG_CAP : 0))
-template <int MODE, bool MSG>
-__global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams p) {
+#define SV_OCTET_LDS_BYTES(MSG, HI) (((HI) ? 2 : 1) * SV_OCTET_TAB_BYTES + ((MSG) ? SV_OSIGS * SV_MSG_CAP : 0))
+// (cached-form table of 0..8 multiples of P, whole on every lane of the quad,
+// into `tab` by the quad's role-0 lane: the decode wave's build, and HI's)
+__device__ __forceinline__ void sv_oct_build_table(uint32_t* tab, const ge_p3& Pt, const qd_role& q, uint32_t role) {
+  ge_cached c1, ce;
+  ge_p3_to_cached(c1, Pt);
+  ge_cached_identity(ce);
+  const bool store = role == 0;
+  if (store) sv_store_lentry((sv_u4*)tab, ce);
+  if (store) sv_store_lentry((sv_u4*)(tab + SV_QENT_DW), c1);
+  // entries 2..8 by repeated addition of P, each addition split over the
+  // quad (qd_add: one product per lane and stage) instead of one lane's
+  // serial 8 products
+  fe mine;
+  fe_pick4(mine, q, c1.T2d, c1.Z, c1.YpX, c1.YmX);
+  ge_p3 P3 = Pt;
+  SV_NOUNROLL for (int e = 2; e < SV_ATAB_ENTRIES; ++e) {
+    qd_add(P3, mine, q, false, true);
+    ge_p3_to_cached(ce, P3);
+    if (store) sv_store_lentry((sv_u4*)(tab + e * SV_QENT_DW), ce);
+  }
+}
+template <int MODE, bool MSG, bool HI>
+__global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams p) {
   // (16-byte aligned: the tables and the message windows are read as sv_u4)
   extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
   static_assert(SV_OCTET_TAB_BYTES % 16 == 0, "the message windows follow the tables at a 16-byte boundary");
   uint32_t(*s_tab)[2][SV_ATAB_ENTRIES][SV_QENT_DW] = (uint32_t(*)[2][SV_ATAB_ENTRIES][SV_QENT_DW])s_dyn;
+  // (HI: the tables of Q = 16^Wlo P after them)
+  uint32_t(*s_tabh)[2][SV_ATAB_ENTRIES][SV_QENT_DW] =
+      (uint32_t(*)[2][SV_ATAB_ENTRIES][SV_QENT_DW])(s_dyn + SV_OCTET_TAB_BYTES / 4);
   __builtin_amdgcn_s_setprio(3);  // latency class (as sv_comb_kernel)
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t role = lane & 3u, half = (lane >> 2) & 1u, sl = lane >> 3;
@@ -535,14 +574,64 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
   // wave-uniform, and visibly so to the compiler (a scalar branch): a
   // divergent-looking branch would be structurized with EXEC masking and
   // both waves would then execute both barriers
-  const bool dec_wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool dec_wave = wv == 1;
+  const bool hi_wave = HI && wv == 2;
+  // HI: the decoded points (decode wave -> high wave), the digit strings and
+  // the window split (wave 0 -> high wave), the high part (high wave -> wave 0)
+  __shared__ uint32_t s_pt[HI ? SV_OSIGS : 1][2][40];
+  __shared__ uint32_t s_hd[HI ? SV_OSIGS : 1][2][9];  // dg[8], flags (1 top8, 2 flip)
+  __shared__ int32_t s_win[2];                         // W, Wlo
+  __shared__ uint32_t s_phi[HI ? SV_OSIGS : 1][2][SV_QENT_DW];
+  if (hi_wave) {
+    __syncthreads();  // the decoded points, digits and split
+    const int W = s_win[0], Wlo = s_win[1];
+    fe h;
+    {
+      const uint32_t* src = &s_pt[sl][half][10 * role];  // own form: lane r holds coordinate r
+      SV_UNROLL for (int k = 0; k < 10; ++k) h.v[k] = src[k];
+    }
+    SV_NOUNROLL for (int k = 0; k < 4 * Wlo; ++k) qo_dbl(h, q);
+    ge_p3 Q;
+    qo_expand(Q, h);
+    uint32_t* tabh = &s_tabh[sl][half][0][0];
+    sv_oct_build_table(tabh, Q, q, role);
+    // (this wave reads back what its role-0 lanes stored: LDS is in order
+    // within a wave)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t dg[8];
+    SV_UNROLL for (int k = 0; k < 8; ++k) dg[k] = s_hd[sl][half][k];
+    const uint32_t fl = s_hd[sl][half][8];
+    const bool top8 = (fl & 1u) != 0, flip = (fl & 2u) != 0;
+    qo_identity(h, q);
+    SV_NOUNROLL for (int w = W - 1; w >= Wlo; --w) {
+      int32_t d = sc_pop_top(dg, 4);
+      if (w == W - 1 && top8) d = 8;
+      if (flip) d = -d;
+      if (w != W - 1) {
+        SV_NOUNROLL for (int k = 0; k < 4; ++k) qo_dbl(h, q);
+      }
+      fe m;
+      qo_load_cached(m, tabh + (d < 0 ? -d : d) * SV_QENT_DW, role, d < 0);
+      qo_add(h, m, q, d < 0);
+    }
+    ge_p3 PH;
+    qo_expand(PH, h);
+    ge_cached ch;
+    ge_p3_to_cached(ch, PH);
+    if (role == 0) sv_store_lentry((sv_u4*)&s_phi[sl][half][0], ch);
+    __syncthreads();  // the high parts written
+    return;
+  }
   uint32_t A[8], S[8], hram[16], R[8];
   if (dec_wave) {
     sv_unpack2(A, p.pk + 2 * ii);
     sv_unpack2(R, p.sig + 4 * ii);
   } else {
     if (MSG) {
-      sv_u4* s_msg = (sv_u4*)(s_dyn + SV_OCTET_TAB_BYTES / 4);
+      sv_u4* s_msg = (sv_u4*)(s_dyn + (HI ? 2 : 1) * SV_OCTET_TAB_BYTES / 4);
       sv_load_and_hash_lds<MODE, 8>(p, ii, lane & 7u, s_msg + sl * (SV_MSG_CAP / 16), A, S, hram);
     } else {
       sv_load_and_hash<MODE>(p, ii, A, S, hram);
@@ -559,6 +648,14 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     // (the DPP read outside the branch: a lane disabled by EXEC is no source)
     const uint32_t both = dok & oc_from_hi(dok);
     if (half == 0 && role == 0) s_dok[sl] = both;
+    if (HI && role == 0) {  // (the high wave's starting point)
+      SV_UNROLL for (int k = 0; k < 10; ++k) {
+        s_pt[sl][half][k] = Pt.X.v[k];
+        s_pt[sl][half][10 + k] = Pt.Y.v[k];
+        s_pt[sl][half][20 + k] = Pt.Z.v[k];
+        s_pt[sl][half][30 + k] = Pt.T.v[k];
+      }
+    }
     ge_cached c1, ce;
     ge_p3_to_cached(c1, Pt);
     ge_cached_identity(ce);
@@ -630,8 +727,18 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
   const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
+  // (HI: this wave runs windows Wlo-1 .. 0, the high wave the rest)
+  const int Wlo = HI ? W - sv_oct_hi_windows(W) : W;
   if (role == 0) {
     SV_UNROLL for (int j = 0; j < SV_LB_DIGITS; ++j) s_bd[sl][half][j] = half ? D.dB1[j] : D.dB0[j];
+    if (HI) {
+      SV_UNROLL for (int k = 0; k < 8; ++k) s_hd[sl][half][k] = half ? D.dR[k] : D.dA[k];
+      s_hd[sl][half][8] = ((half ? D.top8R : D.top8A) ? 1u : 0u) | ((half && D.rneg) ? 2u : 0u);
+    }
+  }
+  if (HI && lane == 0) {
+    s_win[0] = W;
+    s_win[1] = Wlo;
   }
   __syncthreads();  // tables visible to the whole quad
   ok = ok && s_dok[sl] != 0;
@@ -645,14 +752,15 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
   // own form (quad.h): lane r holds coordinate r of P until the end
   fe h;
   qo_identity(h, q);
-  SV_NOUNROLL for (int w = W - 1; w >= 0; --w) {
+  SV_NOUNROLL for (int k = 0; k < W - Wlo; ++k) (void)sc_pop_top(dg, 4);  // (the high wave's digits)
+  SV_NOUNROLL for (int w = Wlo - 1; w >= 0; --w) {
     int32_t d = sc_pop_top(dg, 4);
     if (w == W - 1 && top8) d = 8;
     if (flip) d = -d;
     const bool bwin = false;  // (the base part runs on wave 1)
     const int32_t dB = 0;
     fe b;
-    if (w != W - 1) {
+    if (w != Wlo - 1) {
       SV_NOUNROLL for (int k = 0; k < 4; ++k) qo_dbl(h, q);
     }
     fe m;
@@ -664,6 +772,12 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
   qo_expand(P, h);
   // quad 0: P_A + P_R, P_R in cached form from quad 1
   {
+    if (HI) {
+      __syncthreads();  // [s]B from wave 1, the high parts from wave 2
+      fe mh;
+      qd_load_cached(mh, &s_phi[sl][half][0], role, false);
+      qd_add(P, mh, q, false, true);  // this quad's low + high part
+    }
     ge_p3 PR;
     fe_from_hi(PR.X, P.X);
     fe_from_hi(PR.Y, P.Y);
@@ -676,7 +790,7 @@ __global__ __launch_bounds__(SV_OCTET_BLOCK, 1) void sv_octet_kernel(sv_kparams 
     fe_sub(ymx, PR.Y, PR.X);
     fe_pick4(mine, q, t2d, PR.Z, ypx, ymx);  // role 0 2dT, 1 Z, 2 Y+X, 3 Y-X (qd_add's operand order)
     qd_add(P, mine, q, false, true);
-    __syncthreads();  // [s]B from wave 1
+    if (!HI) __syncthreads();  // [s]B from wave 1
     qd_load_cached(mine, &s_pb[sl][0], role, false);
     qd_add(P, mine, q, false, false);
   }
@@ -1121,13 +1235,21 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
   if (path == 2) {  // SV_PATH_LATENCY
     const unsigned og = (unsigned)((n + SV_OSIGS - 1) / SV_OSIGS);
     const bool msg = og <= sv_device_simds() / 4;
-#define SV_OCTET_LAUNCH(M, G) \
-  hipLaunchKernelGGL((sv_octet_kernel<M, G>), dim3(og), dim3(SV_OCTET_BLOCK), SV_OCTET_LDS_BYTES(G), s, p)
-    if (mode == 0) SV_OCTET_LAUNCH(0, false);  // (32-byte messages: no window)
-    else if (mode == 1 && msg) SV_OCTET_LAUNCH(1, true);
-    else if (mode == 1) SV_OCTET_LAUNCH(1, false);
-    else if (msg) SV_OCTET_LAUNCH(2, true);
-    else SV_OCTET_LAUNCH(2, false);
+    const bool hi = (dbg & SV_KP_OCT_HI) != 0;
+#define SV_OCTET_LAUNCH(M, G, H)                                                                            \
+  hipLaunchKernelGGL((sv_octet_kernel<M, G, H>), dim3(og), dim3((H) ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK), \
+                     SV_OCTET_LDS_BYTES(G, H), s, p)
+#define SV_OCTET_LAUNCH2(M, G) \
+  do {                          \
+    if (hi) SV_OCTET_LAUNCH(M, G, true); \
+    else SV_OCTET_LAUNCH(M, G, false);   \
+  } while (0)
+    if (mode == 0) SV_OCTET_LAUNCH2(0, false);  // (32-byte messages: no window)
+    else if (mode == 1 && msg) SV_OCTET_LAUNCH2(1, true);
+    else if (mode == 1) SV_OCTET_LAUNCH2(1, false);
+    else if (msg) SV_OCTET_LAUNCH2(2, true);
+    else SV_OCTET_LAUNCH2(2, false);
+#undef SV_OCTET_LAUNCH2
 #undef SV_OCTET_LAUNCH
     return hipGetLastError();
   }
