@@ -372,18 +372,22 @@ np.savez(sys.argv[3], **res)
 """
 
 
-def test_staged_fallbacks_keyed_and_bulk(sv, gpu, oracle, tmp_path):
-    """SV_LAT_ZC_IN=0, SV_LAT_ZERO_COPY=0 and SV_BULK_ZC_IN=0 (the staged
-    fallbacks; env switches are read once per process, hence a child): keyed
-    and unkeyed lane and one-chunk bulk batches, and the pieced progress path,
-    against the oracle's verdicts and hashlib's BLAKE2b-256 keys."""
+@pytest.mark.parametrize("variant", ["staged", "alternates"])
+def test_staged_fallbacks_keyed_and_bulk(sv, gpu, oracle, tmp_path, variant):
+    """staged: SV_LAT_ZC_IN=0, SV_LAT_ZERO_COPY=0 and SV_BULK_ZC_IN=0 (the
+    staged fallbacks); alternates: one lane context (SV_LAT_CONTEXTS=1), the
+    two-wave cold octet kernel (SV_OCT_HI_MAX=0) and copied bulk verdicts
+    (SV_BULK_ZC_OUT=0).  Env switches are read once per process, hence a
+    child: keyed and unkeyed lane and one-chunk bulk batches, and the pieced
+    progress path, against the oracle's verdicts and hashlib's BLAKE2b-256 keys."""
     import hashlib
     d = _scp_set(oracle, 1000, seed=78)
     src = tmp_path / "set.npz"
     np.savez(src, pk=d["pk"], sig=d["sig"], msg=d["msg"], msg_off=d["msg_off"].astype(np.uint64),
              msg_len=d["msg_len"].astype(np.uint32))
     dst = tmp_path / "out.npz"
-    env = dict(os.environ, SV_LAT_ZC_IN="0", SV_LAT_ZERO_COPY="0", SV_BULK_ZC_IN="0")
+    env = dict(os.environ, **({"SV_LAT_ZC_IN": "0", "SV_LAT_ZERO_COPY": "0", "SV_BULK_ZC_IN": "0"} if variant == "staged"
+                              else {"SV_LAT_CONTEXTS": "1", "SV_OCT_HI_MAX": "0", "SV_BULK_ZC_OUT": "0"}))
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", _STAGED_KEYED_CHILD, repo, str(src), str(dst)], env=env,
                        capture_output=True, text=True, timeout=300)
