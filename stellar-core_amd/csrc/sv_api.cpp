@@ -1452,6 +1452,14 @@ size_t oct_hi_max() {
   static const size_t v = env_size("SV_OCT_HI_MAX", 4096);
   return v;
 }
+// Above this many signatures (more octet workgroups than CUs) the third wave
+// takes W / 4 of the windows instead of W / 6 (SV_KP_OCT_HI_WIDE): 4k p50
+// 0.372 -> 0.352 ms, where 1k and 2k are 2-5 us faster with W / 6
+// (profiles/r05/octet_hi/cold_r5an_flags_divisors.jsonl, cold_r5ao_flags.jsonl).
+size_t oct_hi_wide_min() {
+  static const size_t v = env_size("SV_OCT_HI_WIDE_MIN", 2048);
+  return v;
+}
 
 bool lat_in_place() {
   static const bool b = env_size("SV_LAT_ZC_IN", 1) != 0;
@@ -1563,7 +1571,9 @@ int lat_launch_locked(Device& D, LatCtx& c, const HostIn& in, size_t n, uint8_t*
       // (a third wave per workgroup takes the chains' top windows while no
       // bulk work runs: its larger workgroup would not fit the slot a
       // shared-mode bulk launch leaves free)
-      const uint32_t hi = (!bulk_busy && n <= oct_hi_max()) ? SV_KP_OCT_HI : 0u;
+      const uint32_t hi = (!bulk_busy && n <= oct_hi_max())
+                              ? SV_KP_OCT_HI | (n > oct_hi_wide_min() ? SV_KP_OCT_HI_WIDE : 0u)
+                              : 0u;
       SV_HIP(sv_launch_verify(mode, SV_PATH_LATENCY, 1, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, n,
                               d_verdict, nullptr, nullptr, D.btab, dbg | hi, 0, nullptr, c.stream));
     }

@@ -504,19 +504,51 @@ __device__ __forceinline__ void fe_from_hi(fe& o, const fe& f) {
 // wave 0 adds the result at the end (second LDS handoff).
 #define SV_OCTET_BLOCK 128
 // HI (cold batches while no bulk work runs, sv_launch_verify): a third wave
-// per workgroup runs the top windows of the -A / -R chains.  It waits for the
-// decoded points at the table barrier, doubles them 4 Wlo times (Q = 16^Wlo P),
-// builds Q's tables in LDS and runs windows W-1 .. Wlo; wave 0 runs Wlo-1 .. 0
-// and adds the high part at the second barrier.  The third wave repeats the
-// doublings, so what it saves is the additions of its windows: balanced at
-// about W / 9 of them.
+// per workgroup runs the top windows of the -A / -R chains.  It starts as soon
+// as the decode wave has the decoded points (before their tables), doubles
+// them 4 Wlo times (Q = 16^Wlo P), builds Q's tables in LDS and runs windows
+// W-1 .. Wlo; wave 0 runs Wlo-1 .. 0 and adds the high part at the end.  The
+// third wave repeats the doublings, so what it saves is the additions of its
+// windows, plus the head start it gets on wave 0, which waits for the tables:
+// balanced at about W / SV_OCT_HI_DIV of them, W / SV_OCT_HI_DIV_WIDE for
+// launches the host marks SV_KP_OCT_HI_WIDE (more workgroups than CUs, where
+// wave 0 shares its SIMD more often).
+// The waves of a HI workgroup hand over through LDS flags, not barriers (a
+// barrier would hold the third wave until the table build is done): one
+// barrier at entry clears the flags, each hand-over is data, a release fence
+// and a flag store, and each wait an acquire after the flag is seen.
 #define SV_OCTET_BLOCK_HI 192
 #ifndef SV_OCT_HI_DIV
-#define SV_OCT_HI_DIV 9
+#define SV_OCT_HI_DIV 6
 #endif
-__device__ __forceinline__ int sv_oct_hi_windows(int W) {
-  const int h = (W + SV_OCT_HI_DIV / 2) / SV_OCT_HI_DIV;
-  return h < 1 ? 1 : (h > W ? W : h);
+#ifndef SV_OCT_HI_DIV_WIDE
+#define SV_OCT_HI_DIV_WIDE 4
+#endif
+// windows the third wave doubles through before it needs W (wave 0's lattice
+// reduction); a split that would leave wave 0 fewer is not made (tiny W: the
+// high part is then the identity)
+#define SV_OCT_HI_PRE 20
+__device__ __forceinline__ int sv_oct_hi_windows(int W, uint32_t dbg) {
+  const int div = (dbg & SV_KP_OCT_HI_WIDE) ? SV_OCT_HI_DIV_WIDE : SV_OCT_HI_DIV;
+  int h = (W + div / 2) / div;
+  h = h < 1 ? 1 : (h > W ? W : h);
+  return W - h < SV_OCT_HI_PRE ? 0 : h;
+}
+enum { SV_OF_PT = 0, SV_OF_TAB, SV_OF_DIG, SV_OF_PB, SV_OF_PHI, SV_OF_N };
+// hand-over: this wave's LDS writes before the flag
+__device__ __forceinline__ void sv_oflag_set(uint32_t* f) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63u) == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait for a hand-over (bounded: a lost flag ends the wait with wrong
+// verdicts, caught by the tests, instead of a hung kernel)
+__device__ __forceinline__ void sv_oflag_wait(uint32_t* f) {
+  for (uint32_t it = 0; it < (1u << 24); ++it) {
+    const uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__builtin_amdgcn_readfirstlane(v) != 0) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // The tables (23 KB) are dynamic LDS, placed after the static arrays below:
@@ -583,46 +615,57 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
   __shared__ uint32_t s_hd[HI ? SV_OSIGS : 1][2][9];  // dg[8], flags (1 top8, 2 flip)
   __shared__ int32_t s_win[2];                         // W, Wlo
   __shared__ uint32_t s_phi[HI ? SV_OSIGS : 1][2][SV_QENT_DW];
+  __shared__ uint32_t s_oflag[HI ? SV_OF_N : 1];
+  if (HI) {
+    if (threadIdx.x < SV_OF_N) s_oflag[threadIdx.x] = 0;
+    __syncthreads();  // (the only barrier of a HI workgroup)
+  }
   if (hi_wave) {
-    __syncthreads();  // the decoded points, digits and split
-    const int W = s_win[0], Wlo = s_win[1];
+    sv_oflag_wait(&s_oflag[SV_OF_PT]);  // the decoded points
     fe h;
     {
       const uint32_t* src = &s_pt[sl][half][10 * role];  // own form: lane r holds coordinate r
       SV_UNROLL for (int k = 0; k < 10; ++k) h.v[k] = src[k];
     }
-    SV_NOUNROLL for (int k = 0; k < 4 * Wlo; ++k) qo_dbl(h, q);
-    ge_p3 Q;
-    qo_expand(Q, h);
-    uint32_t* tabh = &s_tabh[sl][half][0][0];
-    sv_oct_build_table(tabh, Q, q, role);
-    // (this wave reads back what its role-0 lanes stored: LDS is in order
-    // within a wave)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint32_t dg[8];
-    SV_UNROLL for (int k = 0; k < 8; ++k) dg[k] = s_hd[sl][half][k];
-    const uint32_t fl = s_hd[sl][half][8];
-    const bool top8 = (fl & 1u) != 0, flip = (fl & 2u) != 0;
-    qo_identity(h, q);
-    SV_NOUNROLL for (int w = W - 1; w >= Wlo; --w) {
-      int32_t d = sc_pop_top(dg, 4);
-      if (w == W - 1 && top8) d = 8;
-      if (flip) d = -d;
-      if (w != W - 1) {
-        SV_NOUNROLL for (int k = 0; k < 4; ++k) qo_dbl(h, q);
+    SV_NOUNROLL for (int k = 0; k < 4 * SV_OCT_HI_PRE; ++k) qo_dbl(h, q);
+    sv_oflag_wait(&s_oflag[SV_OF_DIG]);  // the digits and the split
+    const int W = s_win[0], Wlo = s_win[1];
+    if (Wlo < W) {  // (Wlo >= SV_OCT_HI_PRE then, sv_oct_hi_windows)
+      SV_NOUNROLL for (int k = 4 * SV_OCT_HI_PRE; k < 4 * Wlo; ++k) qo_dbl(h, q);
+      ge_p3 Q;
+      qo_expand(Q, h);
+      uint32_t* tabh = &s_tabh[sl][half][0][0];
+      sv_oct_build_table(tabh, Q, q, role);
+      // (this wave reads back what its role-0 lanes stored: LDS is in order
+      // within a wave)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      uint32_t dg[8];
+      SV_UNROLL for (int k = 0; k < 8; ++k) dg[k] = s_hd[sl][half][k];
+      const uint32_t fl = s_hd[sl][half][8];
+      const bool top8 = (fl & 1u) != 0, flip = (fl & 2u) != 0;
+      qo_identity(h, q);
+      SV_NOUNROLL for (int w = W - 1; w >= Wlo; --w) {
+        int32_t d = sc_pop_top(dg, 4);
+        if (w == W - 1 && top8) d = 8;
+        if (flip) d = -d;
+        if (w != W - 1) {
+          SV_NOUNROLL for (int k = 0; k < 4; ++k) qo_dbl(h, q);
+        }
+        fe m;
+        qo_load_cached(m, tabh + (d < 0 ? -d : d) * SV_QENT_DW, role, d < 0);
+        qo_add(h, m, q, d < 0);
       }
-      fe m;
-      qo_load_cached(m, tabh + (d < 0 ? -d : d) * SV_QENT_DW, role, d < 0);
-      qo_add(h, m, q, d < 0);
+    } else {
+      qo_identity(h, q);  // (no high windows: the identity)
     }
     ge_p3 PH;
     qo_expand(PH, h);
     ge_cached ch;
     ge_p3_to_cached(ch, PH);
     if (role == 0) sv_store_lentry((sv_u4*)&s_phi[sl][half][0], ch);
-    __syncthreads();  // the high parts written
+    sv_oflag_set(&s_oflag[SV_OF_PHI]);  // the high parts written
     return;
   }
   uint32_t A[8], S[8], hram[16], R[8];
@@ -656,6 +699,7 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
         s_pt[sl][half][30 + k] = Pt.T.v[k];
       }
     }
+    if (HI) sv_oflag_set(&s_oflag[SV_OF_PT]);
     ge_cached c1, ce;
     ge_p3_to_cached(c1, Pt);
     ge_cached_identity(ce);
@@ -678,7 +722,12 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
   __shared__ int32_t s_bd[SV_OSIGS][2][SV_LB_DIGITS];  // base-point digits (wave 0 -> 1)
   __shared__ uint32_t s_pb[SV_OSIGS][SV_QENT_DW];       // [s]B, cached form (wave 1 -> 0)
   if (dec_wave) {
-    __syncthreads();  // tables and s_dok written; s_bd read below
+    if (HI) {
+      sv_oflag_set(&s_oflag[SV_OF_TAB]);   // tables and s_dok written
+      sv_oflag_wait(&s_oflag[SV_OF_DIG]);  // s_bd
+    } else {
+      __syncthreads();  // tables and s_dok written; s_bd read below
+    }
     {
       // quad 0: [s_lo] B from e B, quad 1: [s_hi] 2^128 B from e 2^128 B;
       // digit j carries weight 2^(16 j) (Horner: 16 doublings between digits)
@@ -713,7 +762,8 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
       ge_p3_to_cached(c1, PB);
       if (half == 0 && role == 0) sv_store_lentry((sv_u4*)&s_pb[sl][0], c1);
     }
-    __syncthreads();  // s_pb written
+    if (HI) sv_oflag_set(&s_oflag[SV_OF_PB]);
+    else __syncthreads();  // s_pb written
     return;
   }
   ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
@@ -728,7 +778,7 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
   // (HI: this wave runs windows Wlo-1 .. 0, the high wave the rest)
-  const int Wlo = HI ? W - sv_oct_hi_windows(W) : W;
+  const int Wlo = HI ? W - sv_oct_hi_windows(W, p.dbg) : W;
   if (role == 0) {
     SV_UNROLL for (int j = 0; j < SV_LB_DIGITS; ++j) s_bd[sl][half][j] = half ? D.dB1[j] : D.dB0[j];
     if (HI) {
@@ -740,7 +790,12 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
     s_win[0] = W;
     s_win[1] = Wlo;
   }
-  __syncthreads();  // tables visible to the whole quad
+  if (HI) {
+    sv_oflag_set(&s_oflag[SV_OF_DIG]);   // digits and the split
+    sv_oflag_wait(&s_oflag[SV_OF_TAB]);  // the tables
+  } else {
+    __syncthreads();  // tables visible to the whole quad
+  }
   ok = ok && s_dok[sl] != 0;
 
   const uint32_t* tab = &s_tab[sl][half][0][0];
@@ -773,7 +828,7 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
   // quad 0: P_A + P_R, P_R in cached form from quad 1
   {
     if (HI) {
-      __syncthreads();  // [s]B from wave 1, the high parts from wave 2
+      sv_oflag_wait(&s_oflag[SV_OF_PHI]);  // the high parts from wave 2
       fe mh;
       qd_load_cached(mh, &s_phi[sl][half][0], role, false);
       qd_add(P, mh, q, false, true);  // this quad's low + high part
@@ -790,7 +845,8 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
     fe_sub(ymx, PR.Y, PR.X);
     fe_pick4(mine, q, t2d, PR.Z, ypx, ymx);  // role 0 2dT, 1 Z, 2 Y+X, 3 Y-X (qd_add's operand order)
     qd_add(P, mine, q, false, true);
-    if (!HI) __syncthreads();  // [s]B from wave 1
+    if (HI) sv_oflag_wait(&s_oflag[SV_OF_PB]);  // [s]B from wave 1
+    else __syncthreads();
     qd_load_cached(mine, &s_pb[sl][0], role, false);
     qd_add(P, mine, q, false, false);
   }

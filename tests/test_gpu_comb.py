@@ -272,6 +272,30 @@ def test_cache_off_is_octet_only(sv, gpu, golden):
         sv.set_key_cache(1024)
 
 
+@pytest.mark.parametrize("flags", ["none", "trivial_pair", "max_windows"])
+@pytest.mark.parametrize("n", [700, 3000])
+def test_cold_three_wave_splits(sv, gpu, golden, n, flags):
+    """Cold latency batches of <= 4096 signatures take the three-wave octet
+    kernel (SV_OCT_HI_MAX): the high wave starts from the decoded points
+    through LDS hand-overs and takes W / 6 of the windows, or W / 4 above
+    2048 signatures (SV_KP_OCT_HI_WIDE).  Both splits, with the forced
+    fallback pair and 64 windows (W up to 64), against the golden verdicts."""
+    f = {"none": 0, "trivial_pair": sv.DBG_TRIVIAL_PAIR, "max_windows": sv.DBG_MAX_WINDOWS}[flags]
+    a, e = golden["adversarial"], golden["lattice_edge"]
+    rows_a = np.arange(n) % len(a["verdict"])
+    rows_e = np.arange(n) % len(e["verdict"])
+    sv.set_key_cache(0)
+    prev = sv.set_debug_flags(f)
+    try:
+        for d, rows in ((a, rows_a), (e, rows_e)):
+            out = _run(sv, d, rows)
+            bad = np.nonzero(out != d["verdict"][rows])[0]
+            assert len(bad) == 0, [(int(i), str(d["class_names"][d["cls"][rows[i]]])) for i in bad[:10]]
+    finally:
+        sv.set_debug_flags(prev)
+        sv.set_key_cache(1024)
+
+
 _STAGED_CHILD = r"""
 import ctypes, os, sys
 import numpy as np
