@@ -21,11 +21,13 @@
 
 #include "verify_core.h"
 
-// value of lane K of this lane's quad (DPP quad_perm broadcast)
+// value of lane K of this lane's quad (DPP quad_perm broadcast; bound_ctrl
+// set, which quad_perm never exercises, lets LLVM fold the move into a VOP2
+// consumer such as the X + Y add of qo_dbl)
 template <int K>
 __device__ __forceinline__ uint32_t qd_from(uint32_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xf, 0xf, true);
 #else
   return v;  // (host pass: never executed)
 #endif
@@ -126,8 +128,8 @@ template <int P0, int P1, int P2, int P3>
 __device__ __forceinline__ void fe_perm(fe& o, const fe& f) {
   SV_UNROLL for (int i = 0; i < 10; ++i) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    o.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)f.v[i], P0 | (P1 << 2) | (P2 << 4) | (P3 << 6), 0xf, 0xf,
-                                               false);
+    o.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)f.v[i], P0 | (P1 << 2) | (P2 << 4) | (P3 << 6), 0xf,
+                                                   0xf, true);
 #else
     o.v[i] = f.v[i];
 #endif
