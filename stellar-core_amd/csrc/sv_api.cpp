@@ -744,13 +744,22 @@ uint64_t pack_offsets(const HostIn& in, size_t lo, size_t r0, size_t r1, uint64_
   }
   return pos;
 }
-// kPart: bytes per helper task (a keyed batch's pieces take smaller ones:
-// the first verify launch waits for the last piece)
-void pack_rows(const HostIn& in, size_t lo, size_t r0, size_t r1, const Image& im, uint8_t* h,
-               size_t kPart = 1u << 20) {
+// Bytes per helper task of a pack of at least 2 MB (SV_PACK_PART); smaller
+// packs take 1 MB tasks.  With 1 MB tasks a 29k-signature batch (3.7 MB) was
+// packed by 3 threads; 256 KB tasks spread it over the pool: host call 0.669-
+// 0.707 -> 0.663-0.675 ms, 50k 0.88-0.92 -> 0.86-0.89 ms, while at 8k (1 MB)
+// waking the pool cost 10 us (profiles/r05/host_call/pack_part/).
+size_t pack_part() {
+  static const size_t v = std::max<size_t>(4096, env_size("SV_PACK_PART", 1u << 18));
+  return v;
+}
+// kPart: bytes per helper task, as above when 0 (a keyed batch's pieces take
+// smaller ones: the first verify launch waits for the last piece)
+void pack_rows(const HostIn& in, size_t lo, size_t r0, size_t r1, const Image& im, uint8_t* h, size_t kPart = 0) {
   const uint64_t* offs = (const uint64_t*)(h + im.o_off);
   const size_t m = r1 - r0;
   const size_t est = im.bytes / std::max<size_t>(1, (im.o_sig / 32)) * m;  // (bytes of these rows, roughly)
+  if (kPart == 0) kPart = est >= (2u << 20) ? pack_part() : (1u << 20);
   const size_t parts = std::max<size_t>(1, std::min<size_t>(pool().size() + 1, est / kPart));
   pool().run(parts, [&](size_t t) {
     const size_t a = r0 + m * t / parts, b = r0 + m * (t + 1) / parts;
