@@ -303,6 +303,11 @@ int sv_set_key_tables(int mode, size_t slots);
  * only: verdicts are unchanged. */
 #define SV_DBG_QUAD 0x20u
 #define SV_DBG_NO_QUAD 0x40u
+/* DROP_HANDOVER (needs SV_TEST_KNOBS=1): the three-wave cold-key octet kernel
+ * never raises its tables' hand-over flag, so its verify wave's bounded wait
+ * (~0.5 s) runs out and every signature of the launch is rejected: the
+ * fail-closed path of a lost hand-over. */
+#define SV_DBG_DROP_HANDOVER 0x80u
 int sv_set_debug_flags(uint32_t flags);
 
 /* Bytes of the slot's kernel workspace / pinned staging currently allocated. */

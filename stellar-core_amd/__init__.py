@@ -72,6 +72,8 @@ EXPORTED_SYMBOLS = (
 DBG_TRIVIAL_PAIR, DBG_MAX_WINDOWS, DBG_FAIL, DBG_PREP_ONLY, DBG_KEY_COLLIDE = 0x1, 0x2, 0x4, 0x8, 0x10
 # throughput-path geometry: one signature per quad of lanes on every launch / never
 DBG_QUAD, DBG_NO_QUAD = 0x20, 0x40
+# three-wave cold octet: the tables' hand-over is dropped (its bounded wait runs out: every signature rejects)
+DBG_DROP_HANDOVER = 0x80
 
 
 class SigVerifyError(RuntimeError):

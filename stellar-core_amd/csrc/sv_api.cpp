@@ -291,7 +291,8 @@ std::atomic<uint32_t> g_dbg{0};          // sv_set_debug_flags
 std::atomic<size_t> g_min_shard{0};      // sv_set_min_shard (0: default)
 std::atomic<uint64_t> g_rr{0};           // round-robin slot for single-slot calls
 
-constexpr uint32_t kKernelDbgMask = SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_PREP_ONLY | SV_DBG_KEY_COLLIDE;
+constexpr uint32_t kKernelDbgMask =
+    SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_PREP_ONLY | SV_DBG_KEY_COLLIDE | SV_DBG_DROP_HANDOVER;
 
 // Batches up to this size take the latency kernel under SV_PATH_AUTO
 // (measured crossover on MI355X).
@@ -2216,13 +2217,15 @@ int sv_set_kernel_path(int path) {
 int sv_set_debug_flags(uint32_t flags) {
   LifeGuard life_;
   if (flags & ~(SV_DBG_TRIVIAL_PAIR | SV_DBG_MAX_WINDOWS | SV_DBG_FAIL | SV_DBG_PREP_ONLY | SV_DBG_KEY_COLLIDE |
-                SV_DBG_QUAD | SV_DBG_NO_QUAD))
+                SV_DBG_QUAD | SV_DBG_NO_QUAD | SV_DBG_DROP_HANDOVER))
     return SV_ERR_INVALID_ARG;
   if ((flags & SV_DBG_QUAD) && (flags & SV_DBG_NO_QUAD)) return SV_ERR_INVALID_ARG;
   // the knobs that change what a call returns (FAIL: every call errs;
-  // PREP_ONLY: no verdicts) only exist for processes that opt in
-  if ((flags & (SV_DBG_FAIL | SV_DBG_PREP_ONLY)) && !test_knobs_enabled())
-    return fail(SV_ERR_INVALID_ARG, "SV_DBG_FAIL / SV_DBG_PREP_ONLY need SV_TEST_KNOBS=1 in the environment");
+  // PREP_ONLY: no verdicts; DROP_HANDOVER: cold three-wave batches reject)
+  // only exist for processes that opt in
+  if ((flags & (SV_DBG_FAIL | SV_DBG_PREP_ONLY | SV_DBG_DROP_HANDOVER)) && !test_knobs_enabled())
+    return fail(SV_ERR_INVALID_ARG,
+                "SV_DBG_FAIL / SV_DBG_PREP_ONLY / SV_DBG_DROP_HANDOVER need SV_TEST_KNOBS=1 in the environment");
   return (int)g_dbg.exchange(flags);
 }
 

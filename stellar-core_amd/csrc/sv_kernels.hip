@@ -42,6 +42,7 @@
 #define SV_DBG_MAX_WINDOWS 2u   // every wave runs 64 windows
 #define SV_DBG_PREP_ONLY 8u     // split path: prep kernel only (profiling; no verdicts)
 #define SV_DBG_KEY_COLLIDE 16u  // per-key tables: every key gets the same fingerprint (collision path)
+#define SV_DBG_DROP_HANDOVER 0x80u  // three-wave octet: the tables' hand-over flag is never raised (fail-closed test)
 __device__ __forceinline__ int sv_wave_windows(int wl, uint32_t dbg) {
   int W = (dbg & SV_DBG_MAX_WINDOWS) ? 64 : SV_LAT_MIN_WINDOWS;
   while (__ballot(wl > W) != 0) ++W;
@@ -535,20 +536,24 @@ __device__ __forceinline__ int sv_oct_hi_windows(int W, uint32_t dbg) {
   return W - h < SV_OCT_HI_PRE ? 0 : h;
 }
 enum { SV_OF_PT = 0, SV_OF_TAB, SV_OF_DIG, SV_OF_PB, SV_OF_PHI, SV_OF_N };
-// hand-over: this wave's LDS writes before the flag
-__device__ __forceinline__ void sv_oflag_set(uint32_t* f) {
+// hand-over: this wave's LDS writes before the flag; good = false marks
+// data computed after a wait of this wave that timed out
+__device__ __forceinline__ void sv_oflag_set(uint32_t* f, bool good = true) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if ((threadIdx.x & 63u) == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if ((threadIdx.x & 63u) == 0) __hip_atomic_store(f, good ? 1u : 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// wait for a hand-over (bounded: a lost flag ends the wait with wrong
-// verdicts, caught by the tests, instead of a hung kernel)
-__device__ __forceinline__ void sv_oflag_wait(uint32_t* f) {
+// wait for a hand-over; true if it came and was good.  Bounded (~0.5 s): a
+// lost flag must not hang the kernel.  Wave 0 rejects the workgroup's
+// signatures unless every hand-over it used was good (fail closed).
+__device__ __forceinline__ bool sv_oflag_wait(uint32_t* f) {
+  uint32_t v = 0;
   for (uint32_t it = 0; it < (1u << 24); ++it) {
-    const uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (__builtin_amdgcn_readfirstlane(v) != 0) break;
+    v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (v != 0) break;
     __builtin_amdgcn_s_sleep(1);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return v == 1;
 }
 
 // The tables (23 KB) are dynamic LDS, placed after the static arrays below:
@@ -621,14 +626,14 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
     __syncthreads();  // (the only barrier of a HI workgroup)
   }
   if (hi_wave) {
-    sv_oflag_wait(&s_oflag[SV_OF_PT]);  // the decoded points
+    bool good = sv_oflag_wait(&s_oflag[SV_OF_PT]);  // the decoded points
     fe h;
     {
       const uint32_t* src = &s_pt[sl][half][10 * role];  // own form: lane r holds coordinate r
       SV_UNROLL for (int k = 0; k < 10; ++k) h.v[k] = src[k];
     }
     SV_NOUNROLL for (int k = 0; k < 4 * SV_OCT_HI_PRE; ++k) qo_dbl(h, q);
-    sv_oflag_wait(&s_oflag[SV_OF_DIG]);  // the digits and the split
+    good = sv_oflag_wait(&s_oflag[SV_OF_DIG]) && good;  // the digits and the split
     const int W = s_win[0], Wlo = s_win[1];
     if (Wlo < W) {  // (Wlo >= SV_OCT_HI_PRE then, sv_oct_hi_windows)
       SV_NOUNROLL for (int k = 4 * SV_OCT_HI_PRE; k < 4 * Wlo; ++k) qo_dbl(h, q);
@@ -665,7 +670,7 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
     ge_cached ch;
     ge_p3_to_cached(ch, PH);
     if (role == 0) sv_store_lentry((sv_u4*)&s_phi[sl][half][0], ch);
-    sv_oflag_set(&s_oflag[SV_OF_PHI]);  // the high parts written
+    sv_oflag_set(&s_oflag[SV_OF_PHI], good);  // the high parts written
     return;
   }
   uint32_t A[8], S[8], hram[16], R[8];
@@ -722,9 +727,10 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
   __shared__ int32_t s_bd[SV_OSIGS][2][SV_LB_DIGITS];  // base-point digits (wave 0 -> 1)
   __shared__ uint32_t s_pb[SV_OSIGS][SV_QENT_DW];       // [s]B, cached form (wave 1 -> 0)
   if (dec_wave) {
+    bool dig_good = true;
     if (HI) {
-      sv_oflag_set(&s_oflag[SV_OF_TAB]);   // tables and s_dok written
-      sv_oflag_wait(&s_oflag[SV_OF_DIG]);  // s_bd
+      if (!(p.dbg & SV_DBG_DROP_HANDOVER)) sv_oflag_set(&s_oflag[SV_OF_TAB]);  // tables and s_dok written
+      dig_good = sv_oflag_wait(&s_oflag[SV_OF_DIG]);  // s_bd
     } else {
       __syncthreads();  // tables and s_dok written; s_bd read below
     }
@@ -762,7 +768,7 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
       ge_p3_to_cached(c1, PB);
       if (half == 0 && role == 0) sv_store_lentry((sv_u4*)&s_pb[sl][0], c1);
     }
-    if (HI) sv_oflag_set(&s_oflag[SV_OF_PB]);
+    if (HI) sv_oflag_set(&s_oflag[SV_OF_PB], dig_good);
     else __syncthreads();  // s_pb written
     return;
   }
@@ -790,9 +796,10 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
     s_win[0] = W;
     s_win[1] = Wlo;
   }
+  bool handed = true;  // (HI: every hand-over wave 0 waits for arrived)
   if (HI) {
-    sv_oflag_set(&s_oflag[SV_OF_DIG]);   // digits and the split
-    sv_oflag_wait(&s_oflag[SV_OF_TAB]);  // the tables
+    sv_oflag_set(&s_oflag[SV_OF_DIG]);             // digits and the split
+    handed = sv_oflag_wait(&s_oflag[SV_OF_TAB]);  // the tables
   } else {
     __syncthreads();  // tables visible to the whole quad
   }
@@ -828,7 +835,7 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
   // quad 0: P_A + P_R, P_R in cached form from quad 1
   {
     if (HI) {
-      sv_oflag_wait(&s_oflag[SV_OF_PHI]);  // the high parts from wave 2
+      handed = sv_oflag_wait(&s_oflag[SV_OF_PHI]) && handed;  // the high parts from wave 2
       fe mh;
       qd_load_cached(mh, &s_phi[sl][half][0], role, false);
       qd_add(P, mh, q, false, true);  // this quad's low + high part
@@ -845,12 +852,12 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
     fe_sub(ymx, PR.Y, PR.X);
     fe_pick4(mine, q, t2d, PR.Z, ypx, ymx);  // role 0 2dT, 1 Z, 2 Y+X, 3 Y-X (qd_add's operand order)
     qd_add(P, mine, q, false, true);
-    if (HI) sv_oflag_wait(&s_oflag[SV_OF_PB]);  // [s]B from wave 1
+    if (HI) handed = sv_oflag_wait(&s_oflag[SV_OF_PB]) && handed;  // [s]B from wave 1
     else __syncthreads();
     qd_load_cached(mine, &s_pb[sl][0], role, false);
     qd_add(P, mine, q, false, false);
   }
-  ok = ok && sv_is_identity(P);
+  ok = ok && handed && sv_is_identity(P);
   const bool owner = half == 0 && role == 0;
   if (active && owner) p.verdict[i] = ok ? 1 : 0;
   const uint64_t bal = __ballot(ok && active && owner);

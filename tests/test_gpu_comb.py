@@ -296,6 +296,33 @@ def test_cold_three_wave_splits(sv, gpu, golden, n, flags):
         sv.set_key_cache(1024)
 
 
+def test_cold_three_wave_lost_handover_fails_closed(sv, gpu, golden):
+    """A hand-over flag that never comes (SV_DBG_DROP_HANDOVER: the decode wave
+    does not raise the tables' flag) ends the verify wave's bounded wait
+    (~0.5 s) and rejects every signature of the launch instead of hanging or
+    accepting; the next launch is exact again."""
+    import time
+    d = golden["valid"]
+    rows = np.arange(min(64, len(d["verdict"])))
+    assert d["verdict"][rows].all()
+    sv.set_key_cache(0)
+    prev = sv.set_debug_flags(sv.DBG_DROP_HANDOVER)
+    try:
+        t = time.perf_counter()
+        out = _run(sv, d, rows)
+        dt = time.perf_counter() - t
+        assert not out.any()
+        assert 0.1 < dt < 30
+    finally:
+        sv.set_debug_flags(prev)
+        sv.set_key_cache(1024)
+    sv.set_key_cache(0)
+    try:
+        assert (_run(sv, d, rows) == 1).all()
+    finally:
+        sv.set_key_cache(1024)
+
+
 _STAGED_CHILD = r"""
 import ctypes, os, sys
 import numpy as np
