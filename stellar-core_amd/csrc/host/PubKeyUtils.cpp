@@ -432,6 +432,18 @@ using Item = PubKeyUtils::VerifyItem;
 constexpr size_t kThreadedWalkMin = 16384;
 // eviction draws queued ahead by a waiting walk at most (8 MB of pairs)
 constexpr size_t kPreDrawMax = size_t(1) << 20;
+// Keyed batches below kThreadedWalkMin with SV_HOST_KEYS=1: the cache keys
+// are hashed on the host pool while this thread waits on the engine's
+// verdicts-only call, and the helper that hashes the last slice walks the
+// cache, instead of the engine's hash kernel sharing the GPU with the verify
+// kernel (the default).
+bool hostKeysBeside() {
+  static const bool b = [] {
+    const char* e = getenv("SV_HOST_KEYS");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return b;
+}
 
 // Per-thread scratch reused across calls: a large batch does not pay fresh
 // page faults for its index, key and pointer arrays every time.
@@ -732,7 +744,40 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
         tC = std::chrono::steady_clock::now();
       };
     int erc;
-    if (E >= kThreadedWalkMin) {
+    if (E < kThreadedWalkMin && hostKeysBeside() && gTestKeyedVerifier.load() == nullptr) {
+      // this thread runs the engine call (task 0 of the pool run); the
+      // helpers hash slices of the keys, and the one that finishes the last
+      // slice walks the cache (phase 1: misses inserted pending) while the
+      // GPU still verifies
+      const size_t H = std::max<size_t>(1, std::min<size_t>(hostPool().size(), E / 64));
+      std::atomic<size_t> left{H};
+      std::exception_ptr walkExc, engExc;
+      hostPool().run(H + 1, [&](size_t t) {
+        if (t == 0) {  // (nothing may leave a task: run() returns only after every task)
+          try {
+            erc = timedBatch(true, E, [&] { return gpuVerify(items, rows, verdict.data(), nullptr, nullptr, &sc); });
+          } catch (...) {
+            engExc = std::current_exception();
+            erc = SV_ERR_INVALID_ARG;
+          }
+          return;
+        }
+        const size_t a = E * (t - 1) / H, b = E * t / H;
+        for (size_t e = a; e < b; ++e) {
+          Item const& it = items[rows[e]];
+          keys[e] = PubKeyUtils::verifySigCacheKey(*it.key, it.signature, it.msg);
+        }
+        if (left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+          try {
+            phase1(E);
+          } catch (...) {
+            walkExc = std::current_exception();
+          }
+        }
+      });
+      if (engExc) std::rethrow_exception(engExc);
+      if (walkExc) std::rethrow_exception(walkExc);
+    } else if (E >= kThreadedWalkMin) {
       // Large batches: the engine call runs on a helper thread and publishes
       // how many keys are in (the engine delivers them in pieces); this thread
       // walks the cache as they land -- the thread whose caches hold the
