@@ -183,6 +183,54 @@ def test_verify_sig_batch_dedup_and_verdicts(host, engine, golden):
     assert _counts(host) == (20, n - 20)
 
 
+_HOST_KEYS_CHILD = r"""
+import ctypes, sys
+import numpy as np
+z = np.load(sys.argv[2], allow_pickle=False)
+h = ctypes.CDLL(sys.argv[1])
+vp = ctypes.c_void_p
+pk, sig, msg, off, ln = (np.ascontiguousarray(z[k]) for k in ("pk", "sig", "msg", "msg_off", "msg_len"))
+n = len(ln)
+h.svh_set_keyed_threshold(ctypes.c_size_t(64))
+h.svh_cache_clear()
+outs = []
+for _ in range(2):
+    h.svh_cache_counts(None, None)
+    out = np.zeros(n, np.uint8)
+    assert h.svh_verify_sig_batch(vp(pk.ctypes.data), vp(sig.ctypes.data), None, vp(msg.ctypes.data),
+                                  vp(off.ctypes.data), vp(ln.ctypes.data), ctypes.c_size_t(n), vp(out.ctypes.data)) == 0
+    hit, miss = ctypes.c_uint64(), ctypes.c_uint64()
+    h.svh_cache_counts(ctypes.byref(hit), ctypes.byref(miss))
+    outs.append((out, hit.value, miss.value))
+np.savez(sys.argv[3], v0=outs[0][0], v1=outs[1][0], c=np.array([outs[0][1], outs[0][2], outs[1][1], outs[1][2]]))
+"""
+
+
+def test_keyed_batch_host_keys_beside_engine(host, golden, tmp_path):
+    """SV_HOST_KEYS=1 (read once per process, hence a child): a keyed batch
+    hashes its cache keys on the host pool while the engine call runs and the
+    last hashing helper walks the cache.  Here the engine has no device, so the
+    call fails over to the CPU path after the walk: verdicts must still equal
+    the golden ones, the first batch must miss every distinct item and the
+    second hit every one (the keys the walk inserted are the cache's keys)."""
+    d = golden["adversarial"]
+    rows = np.arange(len(d["verdict"]))[:300]
+    src = tmp_path / "in.npz"
+    np.savez(src, pk=d["pk"][rows], sig=d["sig"][rows], msg=d["msg"], msg_off=d["msg_off"][rows],
+             msg_len=d["msg_len"][rows])
+    dst = tmp_path / "out.npz"
+    env = dict(os.environ, SV_HOST_KEYS="1")
+    r = subprocess.run([sys.executable, "-c", _HOST_KEYS_CHILD, host._name, str(src), str(dst)], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    z = np.load(dst)
+    want = d["verdict"][rows]
+    assert (z["v0"] == want).all() and (z["v1"] == want).all()
+    eligible = int((d["sig"][rows].shape[1] == 64) * len(rows))
+    hit0, miss0, hit1, miss1 = (int(x) for x in z["c"])
+    assert hit0 + miss0 == eligible and hit1 == eligible and miss1 == 0
+
+
 def test_cache_cleared_during_batch(host, oracle, golden):
     """clearVerifySigCache between a batch's cache walk and the resolve of its
     pending inserts (here: from inside the engine call) must neither touch the
