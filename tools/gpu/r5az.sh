@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r5az
 mkdir -p $O
 cd $R
-timeout -k 10 400 python3 -u -m pytest tests/test_host_mirror.py tests/test_gpu_engine.py -m gpu -x -q --timeout 120 \
+SV_HOST_KEYS=1 timeout -k 10 400 python3 -u -m pytest tests/test_host_mirror.py tests/test_gpu_engine.py -m gpu -x -q --timeout 120 \
     --timeout-method thread > $O/pytest.txt 2>&1
 for r in 1 2 3; do
   for k in 0 1; do
