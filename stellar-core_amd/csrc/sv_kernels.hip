@@ -951,20 +951,33 @@ __global__ __launch_bounds__(64, SV_QUAD_WAVES) void sv_quad_kernel(sv_kparams p
   const bool active = i < p.n;
   const uint64_t ii = active ? i : p.n - 1;  // idle tail quads redo the last item (own slots)
   uint32_t A[8], S[8], hram[16], R[8];
-  if (MSG) sv_load_and_hash_lds<MODE, 4>(p, ii, role, s_msg + sq * (SV_MSG_CAP / 16), A, S, hram);
-  else sv_load_and_hash<MODE>(p, ii, A, S, hram);
-  sv_unpack2(R, p.sig + 4 * ii);
-  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
-            sv_point_canonical(R);
+  bool ok = true;
   sv_lat lat;
-  {
-    uint32_t h[8];
-    sc_reduce512(h, hram);
-    sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
-  }
-  const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
   sv_lat_digits D;
-  sv_lat_prepare(D, lat, S, W);
+  int W = 0;
+  // checks, scalar and lattice reduction, digits (after the hash)
+  auto prologue = [&]() {
+    ok = ok && sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
+         sv_point_canonical(R);
+    {
+      uint32_t h[8];
+      sc_reduce512(h, hram);
+      sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
+    }
+    W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
+    sv_lat_prepare(D, lat, S, W);
+  };
+  if (MSG) {
+    sv_load_and_hash_lds<MODE, 4>(p, ii, role, s_msg + sq * (SV_MSG_CAP / 16), A, S, hram);
+    sv_unpack2(R, p.sig + 4 * ii);
+    prologue();
+  } else {
+    // A and R only: the decode below needs nothing else, so a batch read in
+    // place from host memory starts computing once half of its bytes are
+    // across PCIe; S and the message follow after the decode, with the hash
+    sv_unpack2(A, p.pk + 2 * ii);
+    sv_unpack2(R, p.sig + 4 * ii);
+  }
   // decode: lanes 0, 2 -A, lanes 1, 3 -R; then both tables on the whole quad
   uint32_t* tabA = (uint32_t*)(p.ws + i * SV_QSLOT_QUADS);
   uint32_t* tabR = tabA + SV_ATAB_ENTRIES * SV_QENT;
@@ -985,6 +998,19 @@ __global__ __launch_bounds__(64, SV_QUAD_WAVES) void sv_quad_kernel(sv_kparams p
     fe_from<1>(Pq.Z, Pt.Z);
     fe_from<1>(Pq.T, Pt.T);
     sv_qbuild(tabR, Pq, q, role);
+  }
+  if (!MSG) {
+    sv_unpack2(S, p.sig + 4 * ii + 2);
+    if (MODE == 0) {
+      uint32_t M[8];
+      sv_unpack2(M, (const sv_u4*)(p.msg) + 2 * ii);
+      sha512_ram32(hram, R, A, M);
+    } else if (MODE == 1) {
+      sha512_ram_var(hram, R, A, p.msg + p.msg_off[ii], p.msg_len[ii]);
+    } else {
+      sha512_ram_var(hram, R, A, p.msg + ii * (uint64_t)p.fixed_len, p.fixed_len);
+    }
+    prologue();
   }
   const sv_u4* btab0 = p.btab;
   const sv_u4* btab1 = p.btab + SV_LBTAB_ENTRIES * SV_BTAB_QUADS;
