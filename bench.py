@@ -276,8 +276,9 @@ def in_process_multi_gpu(sv, pk, sig, msg, reps=3):
     n = pk.shape[0]
     out = {"slots": slots, "device_map": os.environ.get("SV_DEVICE_MAP"),
            "what": "one process, sv_ed25519_verify_batch_fixed(device=-1, max_devices=G) from pageable host arrays: "
-                   "G contiguous slices on G device slots (one helper thread each), verdicts gathered into the "
-                   "caller's buffer", "per_G": {}}
+                   "G contiguous slices on G device slots, each driven and packed by the slot's own staging workers "
+                   "(pinned to the GPU's NUMA node), verdicts gathered into the caller's buffer; host_feed: the same "
+                   "host side without kernels (sv_host_feed_probe)", "per_G": {}}
     G = 1
     while G <= min(8, slots):
         N = G * n
@@ -297,9 +298,25 @@ def in_process_multi_gpu(sv, pk, sig, msg, reps=3):
             dt = time.perf_counter() - t1
             ok = ok and bool(np.array_equal(o, want))
             best = dt if best is None else min(best, dt)
-        out["per_G"][str(G)] = {"signatures": N, "ms": best * 1e3, "verifies_per_s": N / best,
-                                "verdicts_ok": ok, "verdict_sha256": hashlib.sha256(o.tobytes()).hexdigest()}
-        log("in-process G=%d: %.3e verifies/s" % (G, N / best))
+        row = {"signatures": N, "ms": best * 1e3, "verifies_per_s": N / best,
+               "verdicts_ok": ok, "verdict_sha256": hashlib.sha256(o.tobytes()).hexdigest()}
+        # the host side alone (sv_host_feed_probe: slices, each slot's staging
+        # workers, pack into pinned staging, H2D; no kernels): what G slots'
+        # host feed delivers against what G GPUs verify
+        feed = {}
+        for upload in (False, True):
+            fb, fs = None, None
+            for _ in range(2):
+                r = sv.host_feed_probe(P, S, M, 32, max_devices=G, upload=upload)
+                if fb is None or r["seconds"] < fb:
+                    fb, fs = r["seconds"], r
+            feed["pack_and_h2d" if upload else "pack_only"] = {"sigs_per_s": N / fb, "GBps": N * 128 / fb / 1e9}
+        feed.update({k: fs[k] for k in ("threads_per_slot", "usable_cpus", "gpu_numa", "staging_numa",
+                                        "pinned_cpus")})
+        row["host_feed"] = feed
+        out["per_G"][str(G)] = row
+        log("in-process G=%d: %.3e verifies/s; host feed %.1f GB/s pack, %.1f GB/s pack+H2D" % (
+            G, N / best, feed["pack_only"]["GBps"], feed["pack_and_h2d"]["GBps"]))
         del P, S, M
         G *= 2
     base = out["per_G"]["1"]["verifies_per_s"]

@@ -46,6 +46,12 @@ extern "C" {
 #define SV_ERR_ALLOC (-4)
 #define SV_ERR_NOT_INIT (-5)
 #define SV_ERR_ALIGN (-6)
+/* A kernel reported that it could not stand behind its verdicts (the
+ * three-wave cold-key octet kernel when one of its bounded LDS hand-over waits
+ * ran out).  Like every error: the verdict buffer is unspecified and the batch
+ * must be re-verified (the C++ mirror re-runs it on the CPU path), never
+ * cached as rejects. */
+#define SV_ERR_KERNEL (-7)
 
 /* Batch options.  A NULL opts pointer means "all defaults". */
 typedef struct sv_opts {
@@ -305,10 +311,31 @@ int sv_set_key_tables(int mode, size_t slots);
 #define SV_DBG_NO_QUAD 0x40u
 /* DROP_HANDOVER (needs SV_TEST_KNOBS=1): the three-wave cold-key octet kernel
  * never raises its tables' hand-over flag, so its verify wave's bounded wait
- * (~0.5 s) runs out and every signature of the launch is rejected: the
- * fail-closed path of a lost hand-over. */
+ * (~0.5 s) runs out: the kernel writes fail-closed rejects and raises its
+ * failure word, and the call returns SV_ERR_KERNEL (the error path of a lost
+ * hand-over). */
 #define SV_DBG_DROP_HANDOVER 0x80u
 int sv_set_debug_flags(uint32_t flags);
+
+/* Host-feed probe (multi-GPU sizing).  Runs the host
+ * side of sv_ed25519_verify_batch_fixed(device = -1, max_devices) over n
+ * signatures -- the contiguous slices, each slot's own staging workers
+ * (pinned to the GPU's NUMA node), the pack into the slot's two pinned
+ * staging slots and, with upload != 0, the H2D copies -- and launches no
+ * kernel: no verdicts.  What the G slots' host side can feed, against the
+ * rate G GPUs verify at. */
+typedef struct sv_feed_stats {
+  uint32_t struct_size;      /* sizeof(sv_feed_stats) */
+  uint32_t slots;            /* slots the batch was sliced over */
+  uint32_t threads_per_slot; /* pack threads per slot (1 slot: the shared pool + caller) */
+  uint32_t usable_cpus;      /* affinity limited by the cgroup CPU quota */
+  double seconds;            /* wall time of the whole feed */
+  int32_t gpu_numa[16];      /* NUMA node of slot g's GPU (-1: unknown) */
+  int32_t staging_numa[16];  /* NUMA node of slot g's first pinned staging page (-1: unknown) */
+  uint32_t pinned_cpus[16];  /* CPUs slot g's workers are pinned to (0: not pinned) */
+} sv_feed_stats;
+int sv_host_feed_probe(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t msg_len, size_t n,
+                       uint32_t max_devices, int upload, sv_feed_stats* out);
 
 /* Bytes of the slot's kernel workspace / pinned staging currently allocated. */
 int sv_workspace_bytes(int device, size_t* bytes);

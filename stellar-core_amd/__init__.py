@@ -54,6 +54,7 @@ SV_ERRORS = {
     -4: "SV_ERR_ALLOC",
     -5: "SV_ERR_NOT_INIT",
     -6: "SV_ERR_ALIGN",
+    -7: "SV_ERR_KERNEL",
 }
 
 EXPORTED_SYMBOLS = (
@@ -65,7 +66,7 @@ EXPORTED_SYMBOLS = (
     "sv_ed25519_verify_batch_gather", "sv_ed25519_verify_batch_gather_cb", "sv_ed25519_verify_batch_cpu", "sv_ed25519_verify_cpu",
     "sv_set_device_map", "sv_set_min_shard", "sv_set_debug_flags", "sv_workspace_bytes", "sv_pinned_bytes",
     "sv_set_key_cache", "sv_key_cache_wait", "sv_key_cache_get_stats", "sv_set_key_tables",
-    "sv_ed25519_verify_batch_gather_progress",
+    "sv_ed25519_verify_batch_gather_progress", "sv_host_feed_probe",
 )
 
 # test knobs (include/stellar_sigverify.h sv_set_debug_flags)
@@ -83,6 +84,12 @@ class SigVerifyError(RuntimeError):
 class sv_opts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("max_devices", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class FeedStats(ctypes.Structure):
+    _fields_ = ([(f, ctypes.c_uint32) for f in ("struct_size", "slots", "threads_per_slot", "usable_cpus")]
+                + [("seconds", ctypes.c_double), ("gpu_numa", ctypes.c_int32 * 16),
+                   ("staging_numa", ctypes.c_int32 * 16), ("pinned_cpus", ctypes.c_uint32 * 16)])
 
 
 class KeyCacheStats(ctypes.Structure):
@@ -147,6 +154,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.sv_key_cache_wait.argtypes = [ctypes.c_int]
     lib.sv_key_cache_get_stats.argtypes = [ctypes.c_int, ctypes.POINTER(KeyCacheStats)]
     lib.sv_lat_last_trace.argtypes = [ctypes.POINTER(ctypes.c_double)]
+    lib.sv_host_feed_probe.argtypes = [vp, vp, vp, ctypes.c_uint32, sz, ctypes.c_uint32, ctypes.c_int,
+                                       ctypes.POINTER(FeedStats)]
     _lib = lib
     return lib
 
@@ -425,6 +434,24 @@ def key_cache_stats(device: int = 0) -> dict:
 
 
 LAT_TRACE_FIELDS = ("plan_pack_us", "h2d_call_us", "launch_us", "d2h_rec_us", "build_us", "sync_us", "total_us", "warm")
+
+
+def host_feed_probe(pk, sig, msg, msg_len: int, max_devices: int = 0, upload: bool = True) -> dict:
+    """The host side of a multi-slot fixed-length batch without kernels
+    (sv_host_feed_probe, include/stellar_sigverify.h): slices, each slot's
+    staging workers, pack into pinned staging, optionally the H2D copies."""
+    pk, sig, msg = (np.ascontiguousarray(x, dtype=np.uint8) for x in (pk, sig, msg))
+    n = pk.reshape(-1, 32).shape[0]
+    if sig.size != 64 * n or msg.size != msg_len * n:
+        raise ValueError("pk/sig/msg row mismatch")
+    st = FeedStats()
+    st.struct_size = ctypes.sizeof(FeedStats)
+    _check(load_library().sv_host_feed_probe(pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, msg_len, n,
+                                             max_devices, 1 if upload else 0, ctypes.byref(st)))
+    G = st.slots
+    return {"seconds": st.seconds, "slots": G, "threads_per_slot": st.threads_per_slot,
+            "usable_cpus": st.usable_cpus, "gpu_numa": list(st.gpu_numa)[:G],
+            "staging_numa": list(st.staging_numa)[:G], "pinned_cpus": list(st.pinned_cpus)[:G]}
 
 
 def lat_last_trace() -> dict:

@@ -22,8 +22,14 @@ namespace sv {
 // (a device slice that packs in parallel) cannot deadlock.
 class Pool {
  public:
-  explicit Pool(unsigned threads) {
-    for (unsigned i = 0; i < threads; ++i) th_.emplace_back([this] { loop(); });
+  // init (optional) runs first on every helper thread (a device slot's
+  // workers pin themselves to the GPU's NUMA node there: sv_api.cpp)
+  explicit Pool(unsigned threads, const std::function<void()>& init = {}) {
+    for (unsigned i = 0; i < threads; ++i)
+      th_.emplace_back([this, init] {
+        if (init) init();
+        loop();
+      });
   }
   ~Pool() {
     {
@@ -34,6 +40,19 @@ class Pool {
     for (auto& t : th_) t.join();
   }
   size_t size() const { return th_.size(); }
+  // Queues fn on a helper thread and returns at once (the caller tracks its
+  // completion itself); with no helper threads fn runs here.
+  void post(std::function<void()> fn) {
+    if (th_.empty()) {
+      fn();
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.emplace_back(std::move(fn));
+    }
+    cv_.notify_one();
+  }
   void run(size_t k, const std::function<void(size_t)>& fn) {
     if (k == 0) return;
     if (k == 1 || th_.empty()) {

@@ -351,6 +351,7 @@ hipError_t sv_launch_comb(int mode, int spw, const void* pk, const void* sig, co
   c.k.ws = nullptr;
   c.k.btab = nullptr;
   c.k.dbg = 0;
+  c.k.status = nullptr;
   c.kslot = kslot;
   c.ktab = ktab;
   c.kstat = kstat;

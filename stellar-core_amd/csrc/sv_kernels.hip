@@ -858,6 +858,10 @@ __global__ __launch_bounds__(HI ? SV_OCTET_BLOCK_HI : SV_OCTET_BLOCK, 1) void sv
     qd_add(P, mine, q, false, false);
   }
   ok = ok && handed && sv_is_identity(P);
+  // a lost hand-over: the rejects below are fail-closed placeholders, and the
+  // launch's failure word tells the host so (one plain store per workgroup;
+  // every writer stores the same code)
+  if (HI && !handed && p.status != nullptr && lane == 0) *(volatile uint32_t*)p.status = SV_KFAIL_HANDOVER;
   const bool owner = half == 0 && role == 0;
   if (active && owner) p.verdict[i] = ok ? 1 : 0;
   const uint64_t bal = __ballot(ok && active && owner);
@@ -1307,8 +1311,9 @@ int sv_share_blocks_per_cu(void) { return sv_share_wps(sv_main_wps()) * 4 / (SV_
 hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, const void* sig, const void* msg,
                             const uint64_t* off, const uint32_t* len, uint32_t fixed_len, uint64_t n,
                             void* verdict, void* bitmap, void* ws, const void* btab, uint32_t dbg, int share,
-                            const sv_ktparams* kt, hipStream_t s) {
+                            const sv_ktparams* kt, uint32_t* status, hipStream_t s) {
   sv_kparams p;
+  p.status = status;
   p.pk = (const sv_u4*)pk;
   p.sig = (const sv_u4*)sig;
   p.msg = (const uint8_t*)msg;

@@ -18,7 +18,16 @@ struct sv_kparams {
   sv_u4* ws;              // workspace: grid threads x SV_SLOT_QUADS (lane-major)
   const sv_u4* btab;      // SV_BTAB_ENTRIES x 9 quads (global copy)
   uint32_t dbg;           // SV_DBG_* test knobs (sv_set_debug_flags), 0 in production; + SV_KP_LAT (keytab.h)
+  // optional (nullptr: none): the launch's failure word.  A kernel that cannot
+  // stand behind its verdicts (the three-wave octet kernel after a hand-over
+  // wait ran out) writes a nonzero SV_KFAIL_* code here; the host, which zeroed
+  // it before the launch, then returns an error for the whole batch instead of
+  // the (fail-closed) rejects: an error is never a reject
+  // (include/stellar_sigverify.h; /root/reference/src/crypto/SecretKey.cpp:461-466
+  // caches every verdict it is given).
+  uint32_t* status;
 };
+#define SV_KFAIL_HANDOVER 1u  // sv_octet_kernel<., ., HI>: a hand-over flag never came
 
 __device__ __forceinline__ void sv_unpack2(uint32_t w[8], const sv_u4* p) {
   const sv_u4 a = p[0], b = p[1];

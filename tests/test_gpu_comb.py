@@ -296,26 +296,89 @@ def test_cold_three_wave_splits(sv, gpu, golden, n, flags):
         sv.set_key_cache(1024)
 
 
-def test_cold_three_wave_lost_handover_fails_closed(sv, gpu, golden):
+def _mirror(sv):
+    import ctypes
+    lib = ctypes.CDLL(sv.HOSTLIB_PATH)
+    lib.svh_last_error_string.restype = ctypes.c_char_p
+    lib.svh_set_cpu_threshold.argtypes = [ctypes.c_size_t]
+    lib.svh_set_keyed_threshold.argtypes = [ctypes.c_size_t]
+    return lib
+
+
+def _mirror_stats(host):
+    import ctypes
+
+    class EngineStats(ctypes.Structure):
+        _fields_ = [("gpu_signatures", ctypes.c_uint64), ("gpu_batches", ctypes.c_uint64),
+                    ("cpu_signatures", ctypes.c_uint64), ("fallbacks", ctypes.c_uint64)]
+    s = EngineStats()
+    host.svh_engine_counts_ex(ctypes.byref(s))
+    h, m = ctypes.c_uint64(), ctypes.c_uint64()
+    host.svh_cache_counts(ctypes.byref(h), ctypes.byref(m))
+    return s, h.value, m.value
+
+
+def _mirror_batch(host, d, rows):
+    import ctypes
+    pk, sig = np.ascontiguousarray(d["pk"][rows]), np.ascontiguousarray(d["sig"][rows])
+    off, ln = np.ascontiguousarray(d["msg_off"][rows]), np.ascontiguousarray(d["msg_len"][rows])
+    msg = np.ascontiguousarray(d["msg"])
+    out = np.full(len(rows), 7, np.uint8)
+    vp = ctypes.c_void_p
+    rc = host.svh_verify_sig_batch(vp(pk.ctypes.data), vp(sig.ctypes.data), None, vp(msg.ctypes.data),
+                                   vp(off.ctypes.data), vp(ln.ctypes.data), ctypes.c_size_t(len(rows)),
+                                   vp(out.ctypes.data))
+    assert rc == 0, host.svh_last_error_string()
+    return out
+
+
+@pytest.mark.parametrize("n", [64, 300])
+def test_cold_three_wave_lost_handover_is_an_error(sv, gpu, golden, n):
     """A hand-over flag that never comes (SV_DBG_DROP_HANDOVER: the decode wave
     does not raise the tables' flag) ends the verify wave's bounded wait
-    (~0.5 s) and rejects every signature of the launch instead of hanging or
-    accepting; the next launch is exact again."""
+    (~0.5 s).  The kernel writes fail-closed rejects AND raises the launch's
+    failure word, so the C-ABI returns SV_ERR_KERNEL instead of rejects
+    (include/stellar_sigverify.h: an error is never a reject).  The C++ mirror's
+    verifySigBatch over the same valid rows (n = 64: host-hashed miss batch;
+    n = 300: the keyed pass, whose cache walk has already run when the error
+    comes back) re-runs them on the CPU path: all true, one fallback, no GPU
+    signature counted, and no false verdict enters the verify cache -- the
+    same rows afterwards are all cache hits, all true
+    (/root/reference/src/crypto/SecretKey.cpp:446-466)."""
     import time
     d = golden["valid"]
-    rows = np.arange(min(64, len(d["verdict"])))
+    rows = np.arange(n)
     assert d["verdict"][rows].all()
+    host = _mirror(sv)
     sv.set_key_cache(0)
+    host.svh_set_cpu_threshold(0)
+    host.svh_set_keyed_threshold(256)
+    host.svh_cache_clear()
+    _mirror_stats(host)
     prev = sv.set_debug_flags(sv.DBG_DROP_HANDOVER)
     try:
         t = time.perf_counter()
-        out = _run(sv, d, rows)
-        dt = time.perf_counter() - t
-        assert not out.any()
-        assert 0.1 < dt < 30
+        with pytest.raises(sv.SigVerifyError, match="SV_ERR_KERNEL"):
+            _run(sv, d, rows)
+        assert 0.1 < time.perf_counter() - t < 30  # (the bounded wait ran)
+        out = _mirror_batch(host, d, rows)
+        assert out.all()
+        s, hits, misses = _mirror_stats(host)
+        assert s.fallbacks == 1 and s.gpu_signatures == 0 and s.cpu_signatures == n, (
+            s.fallbacks, s.gpu_signatures, s.cpu_signatures)
+        assert hits == 0 and misses == n
     finally:
         sv.set_debug_flags(prev)
+        host.svh_set_cpu_threshold(1)
         sv.set_key_cache(1024)
+    try:
+        out = _mirror_batch(host, d, rows)
+        assert out.all()
+        s, hits, misses = _mirror_stats(host)
+        assert hits == n and misses == 0 and s.fallbacks == 0
+    finally:
+        host.svh_cache_clear()
+    # and the next cold launch is exact again
     sv.set_key_cache(0)
     try:
         assert (_run(sv, d, rows) == 1).all()

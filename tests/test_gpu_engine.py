@@ -212,6 +212,52 @@ def test_two_slots_on_one_gpu_ragged(sv, dev, golden):
     assert sv.device_count() >= 1
 
 
+def test_eight_slots_on_one_gpu_slot_workers(sv, dev, golden):
+    """The in-process 8-GPU host feed (VERDICT r5 missing #2) rehearsed on one
+    card: eight logical slots mapped onto GPU 0, each slice driven and packed
+    by its slot's own staging workers (sv_api.cpp slot_pool / shard), at ragged
+    n, variable-length and fixed-length, verdicts and BLAKE2b keys exact; the
+    host-feed probe (no kernels) slices the same way."""
+    sv.set_device_map([0] * 8)
+    try:
+        sv.set_min_shard(1000)
+        assert sv.device_count() == 8
+        d = golden["adversarial"]
+        reps = 20000 // len(d["verdict"]) + 1
+        pk, sig = np.tile(d["pk"], (reps, 1)), np.tile(d["sig"], (reps, 1))
+        off, ln, want = np.tile(d["msg_off"], reps), np.tile(d["msg_len"], reps), np.tile(d["verdict"], reps)
+        for n in (8007, 8 * 1000 + 1, len(want)):
+            out = sv.verify_batch(pk[:n], sig[:n], d["msg"], off[:n], ln[:n])
+            assert np.array_equal(out, want[:n]), n
+        v, k = sv.verify_batch_keyed(pk[:9001], sig[:9001], d["msg"], off[:9001], ln[:9001])
+        assert np.array_equal(v, want[:9001])
+        for j in range(0, 9001, 811):
+            o, l = int(off[j]), int(ln[j])
+            assert k[j].tobytes() == hashlib.blake2b(pk[j].tobytes() + sig[j].tobytes() + d["msg"][o:o + l].tobytes(),
+                                                     digest_size=32).digest()
+        v = golden["valid"]
+        rows = np.nonzero(v["msg_len"] == 32)[0]
+        assert len(rows) > 0
+        m32 = np.stack([v["msg"][int(v["msg_off"][i]):int(v["msg_off"][i]) + 32] for i in rows])
+        r = 16384 // len(rows) + 1
+        out = sv.verify_fixed(np.tile(v["pk"][rows], (r, 1)), np.tile(v["sig"][rows], (r, 1)), np.tile(m32, (r, 1)), 32)
+        assert out.all()
+        for s in range(8):
+            assert sv.pinned_bytes(s) > 0, s  # every slot staged a slice
+        n = 8 * 4096
+        rng = np.random.default_rng(3)
+        P = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        S = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+        M = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        for upload in (False, True):
+            st = sv.host_feed_probe(P, S, M, 32, max_devices=8, upload=upload)
+            assert st["slots"] == 8 and st["threads_per_slot"] >= 1 and st["seconds"] > 0, st
+    finally:
+        sv.set_min_shard(0)
+        sv.set_device_map([])
+    assert sv.device_count() >= 1
+
+
 # ------------------------------------------------ engine errors
 def _host(sv):
     lib = ctypes.CDLL(sv.HOSTLIB_PATH)
