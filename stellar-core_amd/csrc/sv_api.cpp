@@ -29,6 +29,7 @@
 // default: a 1k SCP batch stays on one GPU), driven by the persistent helper
 // pool; verdicts land in disjoint ranges of the caller's buffer -- no
 // collective.
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 #include <pthread.h>
 #include <sched.h>
@@ -844,6 +845,36 @@ size_t pack_part() {
   static const size_t v = std::max<size_t>(4096, env_size("SV_PACK_PART", 1u << 18));
   return v;
 }
+// Pack stores bypass the CPU caches (SV_PACK_NT, default on): the pinned
+// image is read by the GPU (DMA or in place), never again by the CPU, and a
+// cached store first reads each destination line.  Measured on the GPU box's
+// host, 128 MB copies: 16 threads 107 -> 180 GB/s, 8 threads 90 -> 127 GB/s
+// (tools/nt_copy_probe.cpp, profiles/r06/feed/nt_copy_probe.txt).
+bool pack_nt() {
+  static const bool b = env_size("SV_PACK_NT", 1) != 0;
+  return b;
+}
+// dst 16-byte aligned (else memcpy); the caller fences (_mm_sfence) before
+// the data is handed to the device.
+inline void nt_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+  if (((uintptr_t)dst & 15u) != 0) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128((const __m128i*)(src + i));
+    const __m128i b = _mm_loadu_si128((const __m128i*)(src + i + 16));
+    const __m128i c = _mm_loadu_si128((const __m128i*)(src + i + 32));
+    const __m128i d = _mm_loadu_si128((const __m128i*)(src + i + 48));
+    _mm_stream_si128((__m128i*)(dst + i), a);
+    _mm_stream_si128((__m128i*)(dst + i + 16), b);
+    _mm_stream_si128((__m128i*)(dst + i + 32), c);
+    _mm_stream_si128((__m128i*)(dst + i + 48), d);
+  }
+  for (; i + 16 <= n; i += 16) _mm_stream_si128((__m128i*)(dst + i), _mm_loadu_si128((const __m128i*)(src + i)));
+  if (i < n) std::memcpy(dst + i, src + i, n - i);
+}
 // kPart: bytes per helper task, as above when 0 (a keyed batch's pieces take
 // smaller ones: the first verify launch waits for the last piece)
 void pack_rows(const HostIn& in, size_t lo, size_t r0, size_t r1, const Image& im, uint8_t* h, size_t kPart = 0) {
@@ -854,30 +885,40 @@ void pack_rows(const HostIn& in, size_t lo, size_t r0, size_t r1, const Image& i
   sv::Pool& pp = pack_pool();
   const size_t cap = t_pack_parts ? t_pack_parts : pp.size() + 1;
   const size_t parts = std::max<size_t>(1, std::min<size_t>(std::min(pp.size() + 1, cap), est / kPart));
+  const bool nt = pack_nt();
+  auto cp = [nt](uint8_t* d, const uint8_t* s, size_t k) {
+    if (nt) nt_copy(d, s, k);
+    else std::memcpy(d, s, k);
+  };
   pp.run(parts, [&](size_t t) {
     const size_t a = r0 + m * t / parts, b = r0 + m * (t + 1) / parts;
     if (a == b) return;
+    // (the streaming stores of this part are ordered before its completion,
+    // which the pool publishes under a mutex, and so before the upload)
+    struct Fence {
+      bool nt;
+      ~Fence() {
+        if (nt) _mm_sfence();
+      }
+    } fence{nt};
     if (!in.gather()) {
-      std::memcpy(h + 32 * a, in.pk + 32 * (lo + a), 32 * (b - a));
-      std::memcpy(h + im.o_sig + 64 * a, in.sig + 64 * (lo + a), 64 * (b - a));
+      cp(h + 32 * a, in.pk + 32 * (lo + a), 32 * (b - a));
+      cp(h + im.o_sig + 64 * a, in.sig + 64 * (lo + a), 64 * (b - a));
       if (!im.var && !in.off) {
-        std::memcpy(h + im.o_msg + a * (size_t)in.fixed, in.msg + (lo + a) * (size_t)in.fixed,
-                    (b - a) * (size_t)in.fixed);
+        cp(h + im.o_msg + a * (size_t)in.fixed, in.msg + (lo + a) * (size_t)in.fixed, (b - a) * (size_t)in.fixed);
         return;
       }
       if (!im.var) {  // (uniform lengths, found by offset: packed at the fixed stride)
-        for (size_t i = a; i < b; ++i)
-          std::memcpy(h + im.o_msg + i * (size_t)in.fixed, in.msg + in.off[lo + i], in.fixed);
+        for (size_t i = a; i < b; ++i) cp(h + im.o_msg + i * (size_t)in.fixed, in.msg + in.off[lo + i], in.fixed);
         return;
       }
     } else {
       for (size_t i = a; i < b; ++i) {
-        std::memcpy(h + 32 * i, in.ppk[lo + i], 32);
-        std::memcpy(h + im.o_sig + 64 * i, in.psig[lo + i], 64);
+        cp(h + 32 * i, in.ppk[lo + i], 32);
+        cp(h + im.o_sig + 64 * i, in.psig[lo + i], 64);
       }
       if (!im.var) {
-        for (size_t i = a; i < b; ++i)
-          std::memcpy(h + im.o_msg + i * (size_t)in.fixed, in.pmsg[lo + i], in.fixed);
+        for (size_t i = a; i < b; ++i) cp(h + im.o_msg + i * (size_t)in.fixed, in.pmsg[lo + i], in.fixed);
         return;
       }
     }
