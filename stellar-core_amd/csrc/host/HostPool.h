@@ -11,5 +11,7 @@ namespace stellar {
 // Runs range(begin, end) over [0, n) in contiguous pieces on the pool (the
 // calling thread takes part), serially when n < 2 * grain.
 void hostParallelFor(size_t n, size_t grain, std::function<void(size_t, size_t)> const& range);
+// Threads a hostParallelFor can use at once (the pool's helpers and the caller).
+size_t hostPoolThreads();
 
 }  // namespace stellar

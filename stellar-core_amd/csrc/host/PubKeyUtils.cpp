@@ -571,6 +571,8 @@ int gpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, u
 
 }  // namespace
 
+size_t hostPoolThreads() { return hostPool().size() + 1; }
+
 void hostParallelFor(size_t n, size_t grain, std::function<void(size_t, size_t)> const& range) {
   const size_t parts = std::max<size_t>(1, std::min<size_t>(hostPool().size() + 1, n / std::max<size_t>(1, grain)));
   if (parts == 1) {

@@ -263,6 +263,21 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
     // the C structs -> the mirror's C++ objects (a node already holds these
     // objects; the tx set is independent per tx from here on)
     auto marshal = [&](size_t t) {
+      // (a tx holds at most 20 signatures and 20 + 1 + 2 signers: with that
+      // capacity kept, a new set's objects are built in place, never
+      // reallocated -- fresh allocations on the pool's threads, first-touch
+      // faults included, were most of this phase for sets seen once:
+      // profiles/r06/config3/)
+      if (dsigs[t].capacity() < 20) dsigs[t].reserve(20);
+      if (sgn[t].capacity() < 24) sgn[t].reserve(24);
+      // the C structs of a later tx of this range, on their way from memory
+      if (t + 2 < ntx) {
+        const svh_tx& nx = txs[t + 2];
+        const char* a = (const char*)(sigs + nx.sig_off);
+        for (size_t b = 0; b < sizeof(svh_decorated_sig) * nx.nsigs; b += 64) __builtin_prefetch(a + b);
+        const char* g = (const char*)(signers + nx.signer_off);
+        for (size_t b = 0; b < sizeof(svh_signer) * nx.nsigners; b += 64) __builtin_prefetch(g + b);
+      }
       std::memcpy(hashes[t].data(), txs[t].contents_hash, 32);
       dsigs[t].resize(txs[t].nsigs);
       for (uint32_t k = 0; k < txs[t].nsigs; ++k) decoratedInto(dsigs[t][k], sigs[txs[t].sig_off + k]);
