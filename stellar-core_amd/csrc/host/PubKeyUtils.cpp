@@ -22,6 +22,7 @@
 #include "../../../include/stellar_sigverify.h"
 #include "../pool.h"
 #include "HostPool.h"
+#include "KeyMemo.h"
 #include "hashes.h"
 
 namespace stellar {
@@ -513,10 +514,40 @@ void cpuVerify(std::vector<Item> const& items, std::vector<size_t> const& rows, 
   gCpuSigs += rows.size();
 }
 
+// The memo of derived cache keys (KeyMemo.h; SV_KEY_MEMO=0 turns it off).
+bool memoOn() {
+  static const bool b = [] {
+    const char* e = getenv("SV_KEY_MEMO");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return b;
+}
+KeyMemo& keyMemo() {
+  static KeyMemo m;
+  return m;
+}
+// keyed batches of at most this many items leave their GPU-hashed keys in the
+// memo (micro-batches of SCP envelopes, whose verifySig follows on the main
+// thread); larger ones (catchup, tx sets) are not re-verified soon
+constexpr size_t kMemoPutMax = 8192;
+
+// verifySigCacheKey through the memo (64-byte signatures only: a shorter one
+// never reaches the cache, SecretKey.cpp:441-444)
+Hash memoKey(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg) {
+  Hash k;
+  if (memoOn() && sig.size() == 64) {
+    if (keyMemo().find(key.ed25519().data(), sig.data(), msg.data(), msg.size(), k.data())) return k;
+    k = PubKeyUtils::verifySigCacheKey(key, sig, msg);
+    keyMemo().put(key.ed25519().data(), sig.data(), msg.data(), msg.size(), k.data());
+    return k;
+  }
+  return PubKeyUtils::verifySigCacheKey(key, sig, msg);
+}
+
 void hostKeys(std::vector<Item> const& items, std::vector<size_t> const& rows, Hash* keys) {
   parallelFor(rows.size(), 256, [&](size_t i) {
     Item const& it = items[rows[i]];
-    keys[i] = PubKeyUtils::verifySigCacheKey(*it.key, it.signature, it.msg);
+    keys[i] = memoKey(*it.key, it.signature, it.msg);
   });
 }
 
@@ -767,7 +798,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
         const size_t a = E * (t - 1) / H, b = E * t / H;
         for (size_t e = a; e < b; ++e) {
           Item const& it = items[rows[e]];
-          keys[e] = PubKeyUtils::verifySigCacheKey(*it.key, it.signature, it.msg);
+          keys[e] = memoKey(*it.key, it.signature, it.msg);
         }
         if (left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
           try {
@@ -858,6 +889,12 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     if (erc == SV_OK) {
       gGpuSigs += E;
       gGpuBatches += 1;
+      // (the engine's keys only: a test hook's need not be real BLAKE2b keys)
+      if (memoOn() && E <= kMemoPutMax && gTestKeyedVerifier.load() == nullptr)
+        for (size_t e = 0; e < E; ++e) {
+          Item const& it = items[rows[e]];
+          keyMemo().put(it.key->ed25519().data(), it.signature.data(), it.msg.data(), it.msg.size(), keys[e].data());
+        }
       if (trace) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         const auto tD = std::chrono::steady_clock::now();
@@ -978,7 +1015,7 @@ bool verifySig(PublicKey const& key, Signature const& signature, ByteSlice const
   // entry another batch has pending) takes the batch path, which re-derives
   // the key and decides exactly as for a one-item batch
   if (key.type() == PUBLIC_KEY_TYPE_ED25519 && signature.size() == 64) {
-    const Hash k = verifySigCacheKey(key, signature, bin);
+    const Hash k = memoKey(key, ByteSlice(signature), bin);
     std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
     const uint32_t id = gVerifySigCache.find(k);
     if (id != RandomEvictionCache::kNone && gVerifySigCache.at(id).owner == 0) {

@@ -9,6 +9,7 @@ The GPU variants at the bottom run the same checks through the real engine.
 """
 import ctypes
 import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -1077,3 +1078,65 @@ def test_helper_pool_many_runs_then_exit(host):
     r = subprocess.run([sys.executable, "-c", _POOL_STRESS, host._name, stub], stdout=subprocess.PIPE,
                        stderr=subprocess.STDOUT, text=True, timeout=90)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:]
+
+
+_MEMO_CHILD = r"""
+import ctypes, hashlib, json, sys
+import numpy as np
+lib = ctypes.CDLL(sys.argv[1])
+lib.svh_verify_sig.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+lib.svh_cache_keys.restype = ctypes.c_size_t
+lib.svh_cache_seed.argtypes = [ctypes.c_uint]
+lib.svh_set_cpu_threshold.argtypes = [ctypes.c_size_t]
+lib.svh_set_cpu_threshold(1 << 20)  # every miss on the CPU path (no GPU here)
+lib.svh_cache_clear()
+lib.svh_cache_seed(7)
+d = np.load(sys.argv[2], allow_pickle=False)
+rows = list(range(0, len(d["verdict"]), 3))[:180]
+def item(i):
+    o, l = int(d["msg_off"][i]), int(d["msg_len"][i])
+    return d["pk"][i].tobytes(), d["sig"][i].tobytes(), d["msg"][o:o + l].tobytes()
+out = {"verdicts": [], "counts": []}
+def counts():
+    h, m = ctypes.c_uint64(), ctypes.c_uint64()
+    lib.svh_cache_counts(ctypes.byref(h), ctypes.byref(m))
+    out["counts"].append([h.value, m.value])
+for p in range(3):
+    for i in rows:
+        pk, sg, m = item(i)
+        out["verdicts"].append(lib.svh_verify_sig(pk, sg, 64, m, len(m)))
+        # the same signature and key over another message, and another key:
+        # never the memoized key of the original bytes
+        out["verdicts"].append(lib.svh_verify_sig(pk, sg, 64, m + b"x", len(m) + 1))
+        if m:
+            mm = bytearray(m); mm[-1] ^= 1
+            out["verdicts"].append(lib.svh_verify_sig(pk, sg, 64, bytes(mm), len(m)))
+        pk2 = bytearray(pk); pk2[0] ^= 1
+        out["verdicts"].append(lib.svh_verify_sig(bytes(pk2), sg, 64, m, len(m)))
+    counts()
+n = lib.svh_cache_keys(None, 0)
+buf = ctypes.create_string_buffer(32 * n)
+lib.svh_cache_keys(buf, n)
+out["keys"] = hashlib.sha256(buf.raw).hexdigest()
+print(json.dumps(out))
+"""
+
+
+def test_key_memo_keeps_verify_cache_semantics(host, sv, golden, tmp_path):
+    """The key memo (csrc/host/KeyMemo.h) skips re-deriving a cache key from
+    byte-identical (pk, sig, msg) only: with it on and off the same verifySig
+    sequence -- repeats, the same signature over altered messages, altered keys
+    -- gives the same verdicts, the same hit / miss counts and the same cache
+    contents (in the reference's eviction order, SecretKey.cpp:446-466)."""
+    d = golden["msglen"]
+    f = tmp_path / "msglen.npz"
+    np.savez(f, **{k: d[k] for k in ("pk", "sig", "msg", "msg_off", "msg_len", "verdict")})
+    res = {}
+    for memo in ("1", "0"):
+        env = dict(os.environ, SV_KEY_MEMO=memo, SV_NO_TORCH="1")
+        r = subprocess.run([sys.executable, "-c", _MEMO_CHILD, sv.HOSTLIB_PATH, str(f)], env=env,
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[memo] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["1"] == res["0"]
+    assert res["1"]["counts"][1][1] == 0 and res["1"]["counts"][1][0] > 0  # the later passes all hit
