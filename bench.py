@@ -448,7 +448,8 @@ class ScpResult(ctypes.Structure):
                 + [("mean_batch", ctypes.c_double)]
                 + [(k, ctypes.c_uint64) for k in ("gpu_batches", "gpu_signatures", "cpu_signatures", "fallbacks")]
                 + [(k, ctypes.c_double) for k in ("wall_s", "ready_p50_us", "ready_p99_us")]
-                + [("burst_waits", ctypes.c_uint64)])
+                + [("burst_waits", ctypes.c_uint64)]
+                + [("main_busy_s", ctypes.c_double), ("main_call_mean_us", ctypes.c_double)])
 
 
 def scp_envelope_set(sodium, n, seed, adversarial=0.1, validators=100):
@@ -561,6 +562,9 @@ def config4_integrated(sv, sodium, n=48000):
                   "offered_per_s": (burst * 1e6 / interval_us) if interval_us else None,
                   "achieved_per_s": m / d["wall_s"] if d["wall_s"] > 0 else None,
                   "main_hit_ratio": d["main_hits"] / max(1, d["main_hits"] + d["main_misses"]),
+                  # the main thread's verifySig ceiling over the run (calls / time inside them):
+                  # an offered rate above it queues on the main thread whatever the engine does
+                  "main_thread_verifysig_per_s": m / d["main_busy_s"] if d["main_busy_s"] > 0 else None,
                   "verdicts_match_libsodium": bool((out == expect[a:b]).all())})
         return d
 

@@ -234,6 +234,8 @@ typedef struct svh_scp_result {
   double wall_s; /* first submission -> last main-thread verifySig */
   double ready_p50_us, ready_p99_us; /* submit -> the item's batch verified and cached (before its continuations) */
   uint64_t burst_waits;              /* idle flushes that first waited for a burst to end */
+  double main_busy_s;                /* the main thread's time inside verifySig: n / main_busy_s is its ceiling */
+  double main_call_mean_us;          /* mean of one main-thread verifySig call */
 } svh_scp_result;
 int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                 const uint32_t* msg_len, size_t n, const svh_scp_params* params, uint8_t* verdict,

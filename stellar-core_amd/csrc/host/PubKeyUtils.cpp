@@ -526,28 +526,33 @@ KeyMemo& keyMemo() {
   static KeyMemo m;
   return m;
 }
-// keyed batches of at most this many items leave their GPU-hashed keys in the
-// memo (micro-batches of SCP envelopes, whose verifySig follows on the main
-// thread); larger ones (catchup, tx sets) are not re-verified soon
-constexpr size_t kMemoPutMax = 8192;
-
 // verifySigCacheKey through the memo (64-byte signatures only: a shorter one
-// never reaches the cache, SecretKey.cpp:441-444)
-Hash memoKey(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg) {
+// never reaches the cache, SecretKey.cpp:441-444).  store: a key derived here
+// enters the memo (the miss path, where a verification follows anyway; the
+// hit path only reads it: a store there would cost every first-time hit)
+Hash memoKey(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg, bool store) {
   Hash k;
   if (memoOn() && sig.size() == 64) {
     if (keyMemo().find(key.ed25519().data(), sig.data(), msg.data(), msg.size(), k.data())) return k;
     k = PubKeyUtils::verifySigCacheKey(key, sig, msg);
-    keyMemo().put(key.ed25519().data(), sig.data(), msg.data(), msg.size(), k.data());
+    if (store) keyMemo().put(key.ed25519().data(), sig.data(), msg.data(), msg.size(), k.data());
     return k;
   }
   return PubKeyUtils::verifySigCacheKey(key, sig, msg);
 }
 
+// Keys derived for at most this many items at once enter the memo: single
+// verifySig misses (a tx's signatures checked on receipt, then again at
+// nomination and apply) -- not a micro-batch's hundreds, whose stores on the
+// flush worker measured ~0.07 ms later verdicts for config 4's paced SCP
+// bursts (profiles/r06/config4/).
+constexpr size_t kMemoStoreMax = 16;
+
 void hostKeys(std::vector<Item> const& items, std::vector<size_t> const& rows, Hash* keys) {
+  const bool store = rows.size() <= kMemoStoreMax;
   parallelFor(rows.size(), 256, [&](size_t i) {
     Item const& it = items[rows[i]];
-    keys[i] = memoKey(*it.key, it.signature, it.msg);
+    keys[i] = memoKey(*it.key, it.signature, it.msg, store);
   });
 }
 
@@ -798,7 +803,7 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
         const size_t a = E * (t - 1) / H, b = E * t / H;
         for (size_t e = a; e < b; ++e) {
           Item const& it = items[rows[e]];
-          keys[e] = memoKey(*it.key, it.signature, it.msg);
+          keys[e] = memoKey(*it.key, it.signature, it.msg, false);
         }
         if (left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
           try {
@@ -889,12 +894,6 @@ std::vector<bool> verifySigBatch(std::vector<VerifyItem> const& items, std::vect
     if (erc == SV_OK) {
       gGpuSigs += E;
       gGpuBatches += 1;
-      // (the engine's keys only: a test hook's need not be real BLAKE2b keys)
-      if (memoOn() && E <= kMemoPutMax && gTestKeyedVerifier.load() == nullptr)
-        for (size_t e = 0; e < E; ++e) {
-          Item const& it = items[rows[e]];
-          keyMemo().put(it.key->ed25519().data(), it.signature.data(), it.msg.data(), it.msg.size(), keys[e].data());
-        }
       if (trace) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         const auto tD = std::chrono::steady_clock::now();
@@ -1015,7 +1014,7 @@ bool verifySig(PublicKey const& key, Signature const& signature, ByteSlice const
   // entry another batch has pending) takes the batch path, which re-derives
   // the key and decides exactly as for a one-item batch
   if (key.type() == PUBLIC_KEY_TYPE_ED25519 && signature.size() == 64) {
-    const Hash k = memoKey(key, ByteSlice(signature), bin);
+    const Hash k = memoKey(key, ByteSlice(signature), bin, false);
     std::lock_guard<std::mutex> guard(gVerifySigCacheMutex);
     const uint32_t id = gVerifySigCache.find(k);
     if (id != RandomEvictionCache::kNone && gVerifySigCache.at(id).owner == 0) {

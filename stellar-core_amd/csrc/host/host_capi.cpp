@@ -600,6 +600,10 @@ int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
     res->main_p50_us = pct(lm, 0.5);
     res->main_p99_us = pct(lm, 0.99);
     res->main_call_p50_us = pct(mainCallUs, 0.5);
+    double busy = 0;
+    for (double x : mainCallUs) busy += x;
+    res->main_busy_s = busy * 1e-6;
+    res->main_call_mean_us = mainCallUs.empty() ? 0 : busy / (double)mainCallUs.size();
     res->main_hits = hits;
     res->main_misses = misses;
     res->main_mismatches = mismatches;

@@ -555,7 +555,8 @@ class ScpResult(ctypes.Structure):
                 + [("mean_batch", ctypes.c_double)]
                 + [(k, ctypes.c_uint64) for k in ("gpu_batches", "gpu_signatures", "cpu_signatures", "fallbacks")]
                 + [(k, ctypes.c_double) for k in ("wall_s", "ready_p50_us", "ready_p99_us")]
-                + [("burst_waits", ctypes.c_uint64)])
+                + [("burst_waits", ctypes.c_uint64)]
+                + [("main_busy_s", ctypes.c_double), ("main_call_mean_us", ctypes.c_double)])
 
 
 def scp_run(host, d, rows, producers, burst, interval_us, max_batch=8192, max_delay_us=2000, workers=2, policy=0,
