@@ -12,6 +12,7 @@ struct sv_u4;  // (verify_core.h: 16-byte quad)
 #define SV_KP_LAT 0x80000000u
 #define SV_KP_OCT_HI 0x40000000u  // (octet launches) the three-wave variant (sv_kernels.hip sv_octet_kernel HI)
 #define SV_KP_OCT_HI_WIDE 0x20000000u  // (with SV_KP_OCT_HI) the high wave takes more windows
+#define SV_KP_IN_PLACE 0x10000000u  // (throughput launches) the inputs are read in place from mapped host memory
 
 #define SV_KT_TQUADS 90  // table_A: SV_ATAB_ENTRIES x SV_LTAB_QUADS (checked in sv_kernels.hip)
 #define SV_KT_QUADS (SV_KT_TQUADS + 3)                   // + pk (2 quads) + status

@@ -622,6 +622,13 @@ bool bulk_zc_out() {
   static const bool b = env_size("SV_BULK_ZC_OUT", 1) != 0;
   return b;
 }
+// One-chunk throughput launches read in place run the prep kernel in its
+// decode-first order (sv_kernels.hip sv_prep_kernel DF; SV_DECODE_FIRST=0: the
+// device path's order)
+bool decode_first() {
+  static const bool b = env_size("SV_DECODE_FIRST", 1) != 0;
+  return b;
+}
 bool share_now(const Device& D) {
   const int64_t w = share_window_ns();
   return w > 0 && now_ns() - D.lat_last_ns.load(std::memory_order_relaxed) < w;
@@ -705,9 +712,10 @@ bool kt_prepare(Device& D, uint64_t n, sv_ktparams* kt) {
 
 // Launch on D.stream (caller holds D.mu and has set the device).  tables:
 // the launch may use the per-key tables (kt_mode / repeated_keys).
+// kp: SV_KP_* launch hints (SV_KP_IN_PLACE: the inputs are mapped host memory)
 int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig, const void* msg, const uint64_t* off,
                   const uint32_t* len, uint32_t fixed_len, uint64_t n, void* verdict, void* bitmap,
-                  bool tables = false) {
+                  bool tables = false, uint32_t kp = 0) {
   const int rp = resolve_path(path, n);
   const bool share = rp != SV_PATH_LATENCY && share_now(D);
   const unsigned grid = grid_for(D, n, share);
@@ -724,7 +732,8 @@ int launch_locked(Device& D, int mode, int path, const void* pk, const void* sig
     SV_HIP(hipEventRecord(e0, D.stream));
   }
   SV_HIP(sv_launch_verify(mode, geom, grid, pk, sig, msg, off, len, fixed_len, n, verdict, bitmap, D.ws.p, D.btab,
-                          g_dbg.load() & kKernelDbgMask, share ? 1 : 0, kt_on ? &ktp : nullptr, nullptr, D.stream));
+                          (g_dbg.load() & kKernelDbgMask) | (kt_on ? 0u : kp), share ? 1 : 0, kt_on ? &ktp : nullptr,
+                          nullptr, D.stream));
   if (share) D.shared_launches.fetch_add(1, std::memory_order_relaxed);
   if (kt_on) {
     ++D.kt.launches;
@@ -1237,7 +1246,8 @@ int host_slice_locked(Device& D, const HostIn& in, size_t n, uint8_t* verdict, u
         tables = launch_geometry(resolve_path(path, chunk), chunk) == SV_PATH_THROUGHPUT &&
                  (ktm == 1 || (ktm == 2 && repeated_keys(in, n)));
       if ((rc = launch_locked(D, mode, path, d, d + im.o_sig, d + im.o_msg, d_off, d_len, in.fixed, m,
-                              zc_out ? D.z_out.dp : s.d_verdict.p, nullptr, tables != 0)))
+                              zc_out ? D.z_out.dp : s.d_verdict.p, nullptr, tables != 0,
+                              in_place && decode_first() ? SV_KP_IN_PLACE : 0u)))
         return rc;
       trace_at("launched");
     }

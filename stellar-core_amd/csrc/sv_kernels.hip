@@ -187,9 +187,19 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_keybuild_kernel(sv
 }
 
 // KT: per-key tables on (a separate instantiation, so the tables-off path
-// carries none of their code)
-template <int MODE, bool KT>
+// carries none of their code).  DF (decode first; launches whose inputs are
+// read in place from mapped host memory, SV_KP_IN_PLACE): a lane loads A and
+// R, decodes both and builds their tables -- 60 % of the kernel -- and only
+// then loads S and the message and hashes: the half of each row the decode
+// needs crosses PCIe first, and the rest arrives while the decodes run,
+// instead of every wave waiting out its whole row first (the quad kernel's
+// order).  The same checks, combined as one conjunction,
+// so the verdicts are unchanged.  Not with KT (a table-backed A skips its
+// decode) and not for device-resident inputs (the headline path keeps its
+// measured order).
+template <int MODE, bool KT, bool DF = false>
 __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cparams c) {
+  static_assert(!(KT && DF), "decode-first runs without per-key tables");
   const sv_kparams& p = c.k;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // index in the chunk
@@ -206,6 +216,30 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   unsigned long long t_prev = __builtin_amdgcn_s_memtime();
 #endif
   uint32_t A[8], S[8], hram[16], R[8];
+  sv_lat lat;
+  bool ok;
+  uint32_t ks = SV_KT_NONE;
+  if (DF) {
+    sv_unpack2(A, p.pk + 2 * ii);
+    sv_unpack2(R, p.sig + 4 * ii);
+    bool dok;
+    {
+      ge_p3 negA;
+      dok = ge_frombytes(negA, A, true);
+      sv_build_ltab(tabA, negA);
+    }
+    {
+      ge_p3 negR;
+      dok = ge_frombytes(negR, R, true) && dok;
+      sv_build_ltab(tabR, negR);
+    }
+    sv_load_rest_and_hash<MODE>(p, ii, A, R, S, hram);
+    ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(R) && sv_point_canonical(A) &&
+         !sv_small_order(A) && dok;
+    uint32_t h[8];
+    sc_reduce512(h, hram);
+    sc_lattice_reduce(lat, h, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0);
+  } else {
 #ifdef SV_PHASE_PROF
   {
     uint32_t M[8];
@@ -224,7 +258,6 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   SV_PHASE(0);
   // per-key tables: skip A for a wave whose keys all have a built entry
   int a_status = -1;
-  uint32_t ks = SV_KT_NONE;
   if (KT) {
     ks = c.kt.kslot[active ? li : c.cnt - 1];
     bool hit = false;
@@ -239,9 +272,8 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
     if (__ballot(!hit) == 0) a_status = (int)(st & 1u);
     else ks = SV_KT_NONE;
   }
-  sv_lat lat;
 #ifdef SV_PHASE_PROF
-  bool ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
+  ok = sc_is_canonical(S) && !sv_small_order(R) && sv_point_canonical(A) && !sv_small_order(A) &&
             sv_point_canonical(R);
   ge_p3 negA, negR;
   ok = ge_frombytes(negA, A, true) && ok;
@@ -257,8 +289,9 @@ __global__ __launch_bounds__(SV_BLOCK, SV_PREP_WAVES) void sv_prep_kernel(sv_cpa
   sv_build_ltab(tabR, negR);
   SV_PHASE(3);
 #else
-  const bool ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0, a_status);
+  ok = sv_lat_pre(lat, A, R, S, hram, tabA, tabR, (p.dbg & SV_DBG_TRIVIAL_PAIR) != 0, a_status);
 #endif
+  }
   const int W = sv_wave_windows(sv_lat_windows(lat.bits), p.dbg);
   sv_lat_digits D;
   sv_lat_prepare(D, lat, S, W);
@@ -1168,7 +1201,7 @@ static int sv_wps(const void* kernel, std::atomic<int>& cache) {
 }
 static std::atomic<int> g_main_wps{0}, g_prep_wps{0};
 static int sv_main_wps(void) { return sv_wps((const void*)sv_main_kernel<false>, g_main_wps); }
-static int sv_prep_wps(void) { return sv_wps((const void*)sv_prep_kernel<0, false>, g_prep_wps); }
+static int sv_prep_wps(void) { return sv_wps((const void*)sv_prep_kernel<0, false, false>, g_prep_wps); }
 // Shared mode (sv_launch_verify `share`): while latency-class batches are
 // live on the device, the throughput kernels leave one workgroup slot per CU
 // free for them -- the persistent main kernel runs one block per CU fewer
@@ -1378,15 +1411,19 @@ hipError_t sv_launch_verify(int mode, int path, unsigned grid, const void* pk, c
       hipLaunchKernelGGL(sv_keyslot_kernel, dim3(pg), dim3(SV_BLOCK), 0, s, c);
       hipLaunchKernelGGL(sv_keybuild_kernel, dim3(pg), dim3(SV_BLOCK), 0, s, c);
     }
-#define SV_PREP_LAUNCH(M, K) hipLaunchKernelGGL((sv_prep_kernel<M, K>), dim3(pg), dim3(SV_BLOCK), plds, s, c)
+#define SV_PREP_LAUNCH(M, K, F) hipLaunchKernelGGL((sv_prep_kernel<M, K, F>), dim3(pg), dim3(SV_BLOCK), plds, s, c)
     if (kt) {
-      if (mode == 0) SV_PREP_LAUNCH(0, true);
-      else if (mode == 1) SV_PREP_LAUNCH(1, true);
-      else SV_PREP_LAUNCH(2, true);
+      if (mode == 0) SV_PREP_LAUNCH(0, true, false);
+      else if (mode == 1) SV_PREP_LAUNCH(1, true, false);
+      else SV_PREP_LAUNCH(2, true, false);
+    } else if (dbg & SV_KP_IN_PLACE) {
+      if (mode == 0) SV_PREP_LAUNCH(0, false, true);
+      else if (mode == 1) SV_PREP_LAUNCH(1, false, true);
+      else SV_PREP_LAUNCH(2, false, true);
     } else {
-      if (mode == 0) SV_PREP_LAUNCH(0, false);
-      else if (mode == 1) SV_PREP_LAUNCH(1, false);
-      else SV_PREP_LAUNCH(2, false);
+      if (mode == 0) SV_PREP_LAUNCH(0, false, false);
+      else if (mode == 1) SV_PREP_LAUNCH(1, false, false);
+      else SV_PREP_LAUNCH(2, false, false);
     }
 #undef SV_PREP_LAUNCH
     if (!(dbg & SV_DBG_PREP_ONLY)) {

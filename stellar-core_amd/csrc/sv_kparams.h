@@ -55,6 +55,24 @@ __device__ __forceinline__ void sv_load_and_hash(const sv_kparams& p, uint64_t i
   }
 }
 
+// The rest of a signature's inputs once A and R are loaded (the decode-first
+// order of sv_prep_kernel<., ., DF>): S, then the message, and R || A || M
+// hashed.
+template <int MODE>
+__device__ __forceinline__ void sv_load_rest_and_hash(const sv_kparams& p, uint64_t ii, const uint32_t A[8],
+                                                      const uint32_t R[8], uint32_t S[8], uint32_t hram[16]) {
+  sv_unpack2(S, p.sig + 4 * ii + 2);
+  if (MODE == 0) {
+    uint32_t M[8];
+    sv_unpack2(M, (const sv_u4*)(p.msg) + 2 * ii);
+    sha512_ram32(hram, R, A, M);
+  } else if (MODE == 1) {
+    sha512_ram_var(hram, R, A, p.msg + p.msg_off[ii], p.msg_len[ii]);
+  } else {
+    sha512_ram_var(hram, R, A, p.msg + ii * (uint64_t)p.fixed_len, p.fixed_len);
+  }
+}
+
 // The latency kernels' loader (sv_comb_kernel chain waves, sv_octet_kernel
 // hash wave).  Their input image lives in mapped host memory (the lane reads
 // it in place), where every dependent round trip costs ~2 us: a message read

@@ -29,14 +29,14 @@ def main():
     out = {"profile_dir": d, "batch": batch}
     # (round 3: the kernels are instantiated with and without per-key tables,
     # sv_prep_kernel<0, false> / sv_main_kernel<false>; the headline runs without)
-    pat = re.compile(r"sv_verify(_lat)?_kernel<0>|sv_prep_kernel<0(, false)?>|sv_main_kernel(<false>)?\(")
+    pat = re.compile(r"sv_verify(_lat)?_kernel<0>|sv_prep_kernel<0(, false){0,2}>|sv_main_kernel(<false>)?\(")
     # the throughput path may cut one launch into several equal chunks
     # (sv_plan_chunk): chunk size = the prep kernel's grid (one lane per
     # signature), and a launch's value = per-dispatch value x chunks
     chunks = 1
     for f in glob.glob(os.path.join(d, "*", "*_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if re.search(r"sv_prep_kernel<0(, false)?>", r["Kernel_Name"]) and int(r["Grid_Size"]) >= 1024:
+            if re.search(r"sv_prep_kernel<0(, false){0,2}>", r["Kernel_Name"]) and int(r["Grid_Size"]) >= 1024:
                 chunks = max(1, batch // int(r["Grid_Size"]))
                 break
         if chunks > 1:
