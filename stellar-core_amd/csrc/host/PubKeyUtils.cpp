@@ -543,9 +543,12 @@ Hash memoKey(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg, b
 
 // Keys derived for at most this many items at once enter the memo: single
 // verifySig misses (a tx's signatures checked on receipt, then again at
-// nomination and apply) -- not a micro-batch's hundreds, whose stores on the
-// flush worker measured ~0.07 ms later verdicts for config 4's paced SCP
-// bursts (profiles/r06/config4/).
+// nomination and apply) -- not a micro-batch's hundreds.  Stores of a
+// micro-batch's keys measured later verdicts for config 4's paced SCP bursts
+// on the flush worker (~0.07 ms) and still ~0.1 ms when made on the host pool
+// right after the walk, while the GPU verifies; the main thread's verifySig
+// ceiling rose from ~1.0-1.5M/s to 2.4-3.5M/s, but its p50 did not improve
+// (profiles/r06/config4/c4_memo_*.jsonl).
 constexpr size_t kMemoStoreMax = 16;
 
 void hostKeys(std::vector<Item> const& items, std::vector<size_t> const& rows, Hash* keys) {

@@ -19,11 +19,12 @@ def main():
     sodium = bench.load_libsodium()
     for _ in range(runs):
         r = bench.config4_integrated(sv, sodium)
-        out = {"memo": os.environ.get("SV_KEY_MEMO", "1")}
+        out = {"memo": os.environ.get("SV_KEY_MEMO", "1"), "memo_keyed": os.environ.get("SV_MEMO_KEYED", "1")}
         for k, f in r.items():
             if isinstance(f, dict):
                 out[k] = {x: round(f[x], 4) for x in ("verdict_p50_ms", "verdict_p99_ms", "main_p50_ms", "main_p99_ms",
-                                                      "ready_p50_ms", "achieved_per_s", "mean_batch")}
+                                                      "ready_p50_ms", "achieved_per_s", "mean_batch",
+                                                      "main_thread_verifysig_per_s")}
         print(json.dumps(out), flush=True)
 
 
