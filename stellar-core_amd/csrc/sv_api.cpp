@@ -1314,29 +1314,41 @@ int feed_slice(Device& D, const HostIn& in, size_t n, int upload, int* staging_n
   int rc;
   if ((rc = ready_locked(D))) return rc;
   const size_t chunk = std::min(n, stage_chunk());
+  // (the slots' `busy` flags belong to host_slice's pending verdict copies:
+  // the probe tracks its own uploads, and leaves nothing in flight on any
+  // return -- the copy stream is drained before an error is reported)
+  bool pending[2] = {false, false};
+  auto drain = [&] { (void)hipStreamSynchronize(D.h2d); };
   size_t m = 0;
   for (size_t lo = 0, c = 0; lo < n; lo += m, ++c) {
     Stage& s = D.st[c & 1];
-    if (s.busy) {
-      SV_HIP(hipEventSynchronize(s.up));
-      s.busy = false;
+    if (pending[c & 1]) {
+      const hipError_t e = hipEventSynchronize(s.up);
+      pending[c & 1] = false;
+      if (e != hipSuccess) {
+        drain();
+        return hip_fail(e, "feed probe: upload");
+      }
     }
     m = n <= chunk ? n : chunk_len(c, chunk, n - lo);
     size_t msg_total;
     const Image im = image_of(in, lo, m, &msg_total);
-    if ((rc = s.h_in.ensure(im.bytes)) || (upload && (rc = s.d_in.ensure(im.bytes)))) return rc;
+    if ((rc = s.h_in.ensure(im.bytes)) || (upload && (rc = s.d_in.ensure(im.bytes)))) {
+      drain();
+      return rc;
+    }
     pack(in, lo, m, im, (uint8_t*)s.h_in.p);
     if (upload) {
-      SV_HIP(hipMemcpyAsync(s.d_in.p, s.h_in.p, im.bytes, hipMemcpyHostToDevice, D.h2d));
-      SV_HIP(hipEventRecord(s.up, D.h2d));
-      s.busy = true;
+      hipError_t e = hipMemcpyAsync(s.d_in.p, s.h_in.p, im.bytes, hipMemcpyHostToDevice, D.h2d);
+      if (e == hipSuccess) e = hipEventRecord(s.up, D.h2d);
+      if (e != hipSuccess) {
+        drain();
+        return hip_fail(e, "feed probe: upload");
+      }
+      pending[c & 1] = true;
     }
   }
-  for (Stage& s : D.st)
-    if (s.busy) {
-      SV_HIP(hipEventSynchronize(s.up));
-      s.busy = false;
-    }
+  SV_HIP(hipStreamSynchronize(D.h2d));
   if (staging_node) *staging_node = page_numa_node(D.st[0].h_in.p);
   return SV_OK;
 }
