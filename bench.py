@@ -34,6 +34,7 @@ import struct
 import sys
 import threading
 import time
+import traceback
 
 import numpy as np
 
@@ -59,6 +60,16 @@ NOMINAL_PEAK_SURVEY = 9.83e12  # SURVEY.md §8 d7 assumption (quarter-rate); mea
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def leg_failed(result, key, exc):
+    """An optional leg of rank 0 (everything but the timed region and config
+    5's collective) that raised: the error goes into the line under `key`
+    instead of costing the line (an 8-GPU node runs the in-process leg over
+    real devices for the first time)."""
+    log("leg %s failed:" % key)
+    traceback.print_exc()
+    result[key] = {"error": "%s: %s" % (type(exc).__name__, exc)}
 
 
 def seeds_and_msgs(lo, hi):
@@ -721,7 +732,12 @@ def main():
     # card) times a G x 2^20 host batch on 1, 2, 4, 8 slots.
     inproc = None
     if rank == 0 and world == 1 and not args.no_host_api and n == 1 << 20:
-        inproc = in_process_multi_gpu(sv, pk_h, sig_h, msgs.reshape(n, 32))
+        try:
+            inproc = in_process_multi_gpu(sv, pk_h, sig_h, msgs.reshape(n, 32))
+        except Exception as e:
+            holder = {}
+            leg_failed(holder, "in_process_multi_gpu", e)
+            inproc = holder["in_process_multi_gpu"]
 
     result = None
     if rank == 0:
@@ -831,166 +847,172 @@ def main():
     # ---- latency @1k batch (config 4), rank 0 only
     sodium = load_libsodium() if rank == 0 else None
     if rank == 0 and not args.no_latency:
-        if sodium is not None:
-            pks, sigs, lmsgs, expect = scp_latency_set(sodium)
-            src = "SCP-sized 128-384 B messages, 100 validators, 10% adversarial (libsodium-signed, libsodium verdicts)"
-        else:
-            k = 1000
-            pks = [pk_h[i].tobytes() for i in range(k)]
-            sigs = [sig_h[i].tobytes() for i in range(k)]
-            lmsgs = [msgs[32 * i:32 * i + 32].tobytes() for i in range(k)]
-            expect = np.ones(k, np.uint8)
-            src = "first 1000 of the device dataset (32 B messages; libsodium unavailable for SCP-sized set)"
-        pk_a = np.frombuffer(b"".join(pks), np.uint8).reshape(-1, 32)
-        sg_a = np.frombuffer(b"".join(sigs), np.uint8).reshape(-1, 64)
-        # the caller's batch in C-ABI form (message bytes + offsets + lengths),
-        # built once: the timed call is what a C++ caller pays per batch
-        m_len = np.array([len(m) for m in lmsgs], np.uint32)
-        m_off = np.zeros(len(lmsgs), np.uint64)
-        m_off[1:] = np.cumsum(m_len[:-1], dtype=np.uint64)
-        m_buf = np.frombuffer(b"".join(lmsgs), np.uint8)
-        # the timed call is the C-ABI entry point itself, as a C++ caller
-        # (Peer.cpp / HerderImpl) makes it: argument pointers prepared once,
-        # no Python-binding conversions inside the timed region (those are
-        # timed separately as python_binding_p50_ms)
-        clib = sv.load_library()
-        pk_a, sg_a = np.ascontiguousarray(pk_a), np.ascontiguousarray(sg_a)
-        v_out = np.zeros(len(m_len), np.uint8)
-        c_args = [ctypes.c_void_p(a.ctypes.data) for a in (pk_a, sg_a, m_buf, m_off, m_len)]
-        c_out = ctypes.c_void_p(v_out.ctypes.data)
-        c_n = ctypes.c_size_t(len(m_len))
-        c_opts = ctypes.byref(sv.sv_opts(ctypes.sizeof(sv.sv_opts), local, 0, 0))
+        try:
+            if sodium is not None:
+                pks, sigs, lmsgs, expect = scp_latency_set(sodium)
+                src = "SCP-sized 128-384 B messages, 100 validators, 10% adversarial (libsodium-signed, libsodium verdicts)"
+            else:
+                k = 1000
+                pks = [pk_h[i].tobytes() for i in range(k)]
+                sigs = [sig_h[i].tobytes() for i in range(k)]
+                lmsgs = [msgs[32 * i:32 * i + 32].tobytes() for i in range(k)]
+                expect = np.ones(k, np.uint8)
+                src = "first 1000 of the device dataset (32 B messages; libsodium unavailable for SCP-sized set)"
+            pk_a = np.frombuffer(b"".join(pks), np.uint8).reshape(-1, 32)
+            sg_a = np.frombuffer(b"".join(sigs), np.uint8).reshape(-1, 64)
+            # the caller's batch in C-ABI form (message bytes + offsets + lengths),
+            # built once: the timed call is what a C++ caller pays per batch
+            m_len = np.array([len(m) for m in lmsgs], np.uint32)
+            m_off = np.zeros(len(lmsgs), np.uint64)
+            m_off[1:] = np.cumsum(m_len[:-1], dtype=np.uint64)
+            m_buf = np.frombuffer(b"".join(lmsgs), np.uint8)
+            # the timed call is the C-ABI entry point itself, as a C++ caller
+            # (Peer.cpp / HerderImpl) makes it: argument pointers prepared once,
+            # no Python-binding conversions inside the timed region (those are
+            # timed separately as python_binding_p50_ms)
+            clib = sv.load_library()
+            pk_a, sg_a = np.ascontiguousarray(pk_a), np.ascontiguousarray(sg_a)
+            v_out = np.zeros(len(m_len), np.uint8)
+            c_args = [ctypes.c_void_p(a.ctypes.data) for a in (pk_a, sg_a, m_buf, m_off, m_len)]
+            c_out = ctypes.c_void_p(v_out.ctypes.data)
+            c_n = ctypes.c_size_t(len(m_len))
+            c_opts = ctypes.byref(sv.sv_opts(ctypes.sizeof(sv.sv_opts), local, 0, 0))
 
-        def timed(iters, traces=None):
-            lat = []
-            for _ in range(iters):
-                t1 = time.perf_counter()
-                rc = clib.sv_ed25519_verify_batch(c_args[0], c_args[1], c_args[2], c_args[3], c_args[4], c_n, c_out,
-                                                  c_opts)
-                lat.append((time.perf_counter() - t1) * 1e3)
-                if rc != 0:
-                    raise RuntimeError("sv_ed25519_verify_batch: %d" % rc)
-                if traces is not None:
-                    traces.append(sv.lat_last_trace())
-            return np.array(lat), v_out.copy()
+            def timed(iters, traces=None):
+                lat = []
+                for _ in range(iters):
+                    t1 = time.perf_counter()
+                    rc = clib.sv_ed25519_verify_batch(c_args[0], c_args[1], c_args[2], c_args[3], c_args[4], c_n, c_out,
+                                                      c_opts)
+                    lat.append((time.perf_counter() - t1) * 1e3)
+                    if rc != 0:
+                        raise RuntimeError("sv_ed25519_verify_batch: %d" % rc)
+                    if traces is not None:
+                        traces.append(sv.lat_last_trace())
+                return np.array(lat), v_out.copy()
 
-        def timed_py(iters):
-            lat = []
-            for _ in range(iters):
-                t1 = time.perf_counter()
+            def timed_py(iters):
+                lat = []
+                for _ in range(iters):
+                    t1 = time.perf_counter()
+                    sv.verify_batch(pk_a, sg_a, m_buf, m_off, m_len, device=local)
+                    lat.append((time.perf_counter() - t1) * 1e3)
+                return np.array(lat)
+
+            def slow_iterations(lat, traces):
+                # every iteration above 2x p50 with the engine's host-side stages
+                # (sv_lat_last_trace): which stage the time went to
+                p50 = float(np.percentile(lat, 50))
+                slow = [i for i in range(len(lat)) if lat[i] > 2 * p50]
+                med = {k: float(np.median([t[k] for t in traces])) for k in sv.LAT_TRACE_FIELDS}
+                return {"count": len(slow), "of": len(lat), "median_stages_us": med,
+                        "iterations": [dict(index=i, ms=float(lat[i]), **{k: round(v, 1) for k, v in traces[i].items()})
+                                       for i in slow[:20]]}
+
+            # steady state of an SCP flood: the validators' key tables are built
+            # (low-priority stream) after the first batch, then every batch runs
+            # the warm-key comb kernel
+            for _ in range(3):
                 sv.verify_batch(pk_a, sg_a, m_buf, m_off, m_len, device=local)
-                lat.append((time.perf_counter() - t1) * 1e3)
-            return np.array(lat)
+            sv.key_cache_wait(local)
+            timed(5)
+            st0 = sv.key_cache_stats(local)
+            tr_w = []
+            lat, out = timed(args.latency_iters, tr_w)
+            st1 = sv.key_cache_stats(local)
+            lat_py = timed_py(200)
+            warm = st1["warm_batches"] - st0["warm_batches"]
+            # cold keys: key cache off (every batch on the octet kernel, no per-key state)
+            cap0 = st1["capacity"]
+            sv.set_key_cache(0)
+            timed(5)
+            tr_c = []
+            lat_c, out_c = timed(args.latency_iters, tr_c)
+            sv.set_key_cache(cap0)
+            result["latency_1k"] = {
+                "batch": len(pks),
+                "p50_ms": float(np.percentile(lat, 50)),
+                "p99_ms": float(np.percentile(lat, 99)),
+                "iters": args.latency_iters,
+                "key_cache": "warm: %d of %d timed batches ran the comb kernel (100 validator keys cached after the "
+                             "first batch; csrc/comb.h)" % (warm, args.latency_iters),
+                "path": "C-ABI sv_ed25519_verify_batch called directly (ctypes, pointers prepared once), one call per "
+                        "batch on the slot's latency lane (pack into pinned staging + H2D + kernel writing verdicts into "
+                        "mapped pinned memory + sync)",
+                "python_binding_p50_ms": float(np.percentile(lat_py, 50)),
+                "set": src,
+                "verdicts_match_libsodium": bool((out == expect).all()),
+                "slow_iterations": slow_iterations(lat, tr_w),
+            }
+            result["latency_1k_cold_keys"] = {
+                "p50_ms": float(np.percentile(lat_c, 50)),
+                "p99_ms": float(np.percentile(lat_c, 99)),
+                "iters": args.latency_iters,
+                "key_cache": "off (sv_set_key_cache(0)): the octet kernel, no per-key state -- what a batch of "
+                             "never-seen keys gets",
+                "verdicts_match_libsodium": bool((out_c == expect).all()),
+                "slow_iterations": slow_iterations(lat_c, tr_c),
+            }
+            spath_l = sodium_path() if sodium is not None else None
+            if spath_l is not None and not args.no_cpu:
+                thr, _ = host_cpus()
+                one, o1 = cpu_batch_latency(spath_l, pk_a, sg_a, m_buf, m_off, m_len, 1, 5)
+                allc, o2 = cpu_batch_latency(spath_l, pk_a, sg_a, m_buf, m_off, m_len, thr, 21)
+                result["latency_1k"]["cpu_libsodium"] = {
+                    "p50_ms_1thread": one, "p50_ms_all_cores": allc, "threads": thr,
+                    "verdicts_match": bool((o1 == expect).all() and (o2 == expect).all()),
+                    "what": "the same 1000-signature set, one libsodium crypto_sign_verify_detached per signature "
+                            "(oracle/cpu_baseline.c cpubase_sodium_batch, static partition over pthreads)"}
 
-        def slow_iterations(lat, traces):
-            # every iteration above 2x p50 with the engine's host-side stages
-            # (sv_lat_last_trace): which stage the time went to
-            p50 = float(np.percentile(lat, 50))
-            slow = [i for i in range(len(lat)) if lat[i] > 2 * p50]
-            med = {k: float(np.median([t[k] for t in traces])) for k in sv.LAT_TRACE_FIELDS}
-            return {"count": len(slow), "of": len(lat), "median_stages_us": med,
-                    "iterations": [dict(index=i, ms=float(lat[i]), **{k: round(v, 1) for k, v in traces[i].items()})
-                                   for i in slow[:20]]}
+            if sodium is not None and not args.no_config4i:
+                t_c = time.perf_counter()
+                result["config4_integrated"] = config4_integrated(sv, sodium)
+                log("config 4 through the micro-batcher in %.1fs" % (time.perf_counter() - t_c))
 
-        # steady state of an SCP flood: the validators' key tables are built
-        # (low-priority stream) after the first batch, then every batch runs
-        # the warm-key comb kernel
-        for _ in range(3):
-            sv.verify_batch(pk_a, sg_a, m_buf, m_off, m_len, device=local)
-        sv.key_cache_wait(local)
-        timed(5)
-        st0 = sv.key_cache_stats(local)
-        tr_w = []
-        lat, out = timed(args.latency_iters, tr_w)
-        st1 = sv.key_cache_stats(local)
-        lat_py = timed_py(200)
-        warm = st1["warm_batches"] - st0["warm_batches"]
-        # cold keys: key cache off (every batch on the octet kernel, no per-key state)
-        cap0 = st1["capacity"]
-        sv.set_key_cache(0)
-        timed(5)
-        tr_c = []
-        lat_c, out_c = timed(args.latency_iters, tr_c)
-        sv.set_key_cache(cap0)
-        result["latency_1k"] = {
-            "batch": len(pks),
-            "p50_ms": float(np.percentile(lat, 50)),
-            "p99_ms": float(np.percentile(lat, 99)),
-            "iters": args.latency_iters,
-            "key_cache": "warm: %d of %d timed batches ran the comb kernel (100 validator keys cached after the "
-                         "first batch; csrc/comb.h)" % (warm, args.latency_iters),
-            "path": "C-ABI sv_ed25519_verify_batch called directly (ctypes, pointers prepared once), one call per "
-                    "batch on the slot's latency lane (pack into pinned staging + H2D + kernel writing verdicts into "
-                    "mapped pinned memory + sync)",
-            "python_binding_p50_ms": float(np.percentile(lat_py, 50)),
-            "set": src,
-            "verdicts_match_libsodium": bool((out == expect).all()),
-            "slow_iterations": slow_iterations(lat, tr_w),
-        }
-        result["latency_1k_cold_keys"] = {
-            "p50_ms": float(np.percentile(lat_c, 50)),
-            "p99_ms": float(np.percentile(lat_c, 99)),
-            "iters": args.latency_iters,
-            "key_cache": "off (sv_set_key_cache(0)): the octet kernel, no per-key state -- what a batch of "
-                         "never-seen keys gets",
-            "verdicts_match_libsodium": bool((out_c == expect).all()),
-            "slow_iterations": slow_iterations(lat_c, tr_c),
-        }
-        spath_l = sodium_path() if sodium is not None else None
-        if spath_l is not None and not args.no_cpu:
-            thr, _ = host_cpus()
-            one, o1 = cpu_batch_latency(spath_l, pk_a, sg_a, m_buf, m_off, m_len, 1, 5)
-            allc, o2 = cpu_batch_latency(spath_l, pk_a, sg_a, m_buf, m_off, m_len, thr, 21)
-            result["latency_1k"]["cpu_libsodium"] = {
-                "p50_ms_1thread": one, "p50_ms_all_cores": allc, "threads": thr,
-                "verdicts_match": bool((o1 == expect).all() and (o2 == expect).all()),
-                "what": "the same 1000-signature set, one libsodium crypto_sign_verify_detached per signature "
-                        "(oracle/cpu_baseline.c cpubase_sodium_batch, static partition over pthreads)"}
-
-        if sodium is not None and not args.no_config4i:
-            t_c = time.perf_counter()
-            result["config4_integrated"] = config4_integrated(sv, sodium)
-            log("config 4 through the micro-batcher in %.1fs" % (time.perf_counter() - t_c))
-
-        # the bulk configurations below run outside the latency lane's
-        # shared-mode window (SV_LAT_SHARE_MS, csrc/sv_api.cpp share_now)
-        time.sleep(1.1)
+            # the bulk configurations below run outside the latency lane's
+            # shared-mode window (SV_LAT_SHARE_MS, csrc/sv_api.cpp share_now)
+            time.sleep(1.1)
+        except Exception as e:  # (rank 0's optional legs: recorded, never the whole line)
+            leg_failed(result, 'latency_1k', e)
 
     # ---- CPU baseline (rank 0, every N: after the timed region and its final
     # barrier, on the host cores of this job; the other ranks wait at the next
     # collective)
     if rank == 0 and not args.no_cpu:
-        threads, cpu_info = host_cpus()
-        spath = sodium_path() if sodium is not None else None
-        if spath is not None:
-            kind = "reference"
-            sample = min(args.cpu_sample, n)
-            st_sample = min(16384, n)
-            desc = "libsodium %s crypto_sign_verify_detached (dlopen %s), first %d signatures of the bench dataset" % (
-                sodium.sodium_version_string().decode(), spath, sample)
-        else:
-            kind = "port"
-            sample = min(8192, n)
-            st_sample = min(1024, n)
-            desc = "oracle/ C restatement (libsodium unavailable), first %d signatures" % sample
-        rate, dt, out = cpu_verify_rate(pk_h[:sample], sig_h[:sample], msgs[:32 * sample], 32, threads, spath)
-        rate1, dt1, out1 = cpu_verify_rate(pk_h[:st_sample], sig_h[:st_sample], msgs[:32 * st_sample], 32, 1, spath)
-        result["cpu_baseline"] = {
-            "value": rate,
-            "unit": "verifies/s",
-            "cores": threads,
-            "kind": kind,
-            "sample": desc + " (%.2f s wall on %d pthreads, static contiguous partition; native harness "
-                             "oracle/cpu_baseline.c)" % (dt, threads),
-            "single_thread_value": rate1,
-            "host_cpus": cpu_info,
-            "cpu_verdicts_all_valid": bool(out.all() and out1.all()),
-            "gpu_over_cpu": value / rate if rate > 0 else None,
-        }
-        if spath is not None and not args.no_config1:
-            t_c1 = time.perf_counter()
-            result["config1"] = config1(sv, sodium, spath, pk_h, sig_h, msgs, threads, local)
-            log("config 1 (both shapes) in %.1fs" % (time.perf_counter() - t_c1))
+        try:
+            threads, cpu_info = host_cpus()
+            spath = sodium_path() if sodium is not None else None
+            if spath is not None:
+                kind = "reference"
+                sample = min(args.cpu_sample, n)
+                st_sample = min(16384, n)
+                desc = "libsodium %s crypto_sign_verify_detached (dlopen %s), first %d signatures of the bench dataset" % (
+                    sodium.sodium_version_string().decode(), spath, sample)
+            else:
+                kind = "port"
+                sample = min(8192, n)
+                st_sample = min(1024, n)
+                desc = "oracle/ C restatement (libsodium unavailable), first %d signatures" % sample
+            rate, dt, out = cpu_verify_rate(pk_h[:sample], sig_h[:sample], msgs[:32 * sample], 32, threads, spath)
+            rate1, dt1, out1 = cpu_verify_rate(pk_h[:st_sample], sig_h[:st_sample], msgs[:32 * st_sample], 32, 1, spath)
+            result["cpu_baseline"] = {
+                "value": rate,
+                "unit": "verifies/s",
+                "cores": threads,
+                "kind": kind,
+                "sample": desc + " (%.2f s wall on %d pthreads, static contiguous partition; native harness "
+                                 "oracle/cpu_baseline.c)" % (dt, threads),
+                "single_thread_value": rate1,
+                "host_cpus": cpu_info,
+                "cpu_verdicts_all_valid": bool(out.all() and out1.all()),
+                "gpu_over_cpu": value / rate if rate > 0 else None,
+            }
+            if spath is not None and not args.no_config1:
+                t_c1 = time.perf_counter()
+                result["config1"] = config1(sv, sodium, spath, pk_h, sig_h, msgs, threads, local)
+                log("config 1 (both shapes) in %.1fs" % (time.perf_counter() - t_c1))
+        except Exception as e:  # (rank 0's optional legs: recorded, never the whole line)
+            leg_failed(result, 'cpu_baseline', e)
     if not args.no_config35 and n == 1 << 20 and 64 % world == 0:
         t_c = time.perf_counter()
         c5 = config5(sv, torch, dev, stream, local, d_pk, d_sig, d_msg, n, world, rank, barrier, dist)
@@ -999,7 +1021,10 @@ def main():
             log("config 5 (64M signatures on %d GPU(s)) in %.1fs" % (world, time.perf_counter() - t_c))
     if rank == 0 and not args.no_config35 and n == 1 << 20:
         t_c = time.perf_counter()
-        result["config3"] = config3()
+        try:
+            result["config3"] = config3()
+        except Exception as e:
+            leg_failed(result, "config3", e)
         log("config 3 (5000-tx set) in %.1fs" % (time.perf_counter() - t_c))
 
     if rank == 0:
