@@ -2249,7 +2249,7 @@ int sv_device_count(void) {
 const char* sv_last_error_string(void) { return t_err.c_str(); }
 
 const char* sv_version(void) {
-  return "stellar-core_amd sigverify r4 (gfx950; ed25519 == libsodium-1.0.18 crypto_sign_verify_detached)";
+  return "stellar-core_amd sigverify r6 (gfx950; ed25519 == libsodium-1.0.18 crypto_sign_verify_detached)";
 }
 
 int sv_ed25519_verify_batch(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
