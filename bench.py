@@ -446,7 +446,7 @@ def scp_latency_set(sodium, n=1000, adversarial=0.1, seed=20250211):
 class ScpParams(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint32) for k in ("struct_size", "producers", "burst", "interval_us", "max_batch",
                                                "max_delay_us", "workers", "policy", "linger_us", "idle_in_flight",
-                                               "quiet_us", "max_linger_us")]
+                                               "quiet_us", "max_linger_us", "batch_post")]
 
 
 class ScpResult(ctypes.Structure):
@@ -547,11 +547,11 @@ def config4_integrated(sv, sodium, n=48000):
     gen_s = time.perf_counter() - t0
 
     def run(sl, producers, burst, interval_us, workers=2, policy=0, linger_us=0, max_batch=8192,
-            max_delay_us=2000, quiet_us=0, max_linger_us=200):
+            max_delay_us=2000, quiet_us=0, max_linger_us=200, batch_post=0):
         a, b = sl
         m = b - a
         p = ScpParams(ctypes.sizeof(ScpParams), producers, burst, interval_us, max_batch, max_delay_us, workers,
-                      policy, linger_us, 1, quiet_us, max_linger_us)
+                      policy, linger_us, 1, quiet_us, max_linger_us, batch_post)
         r = ScpResult()
         out = np.full(m, 7, np.uint8)
         o0 = int(off[a])
@@ -569,6 +569,7 @@ def config4_integrated(sv, sodium, n=48000):
         d.update({"envelopes": m, "producers": producers, "burst": burst, "interval_us": interval_us,
                   "workers": workers, "policy": "deadline" if policy else "when_idle", "linger_us": linger_us,
                   "quiet_us": quiet_us, "max_linger_us": max_linger_us,
+                  "main_thread_post": "one task per verified batch" if batch_post else "one task per envelope",
                   "max_batch_setting": max_batch, "max_delay_us": max_delay_us,
                   "offered_per_s": (burst * 1e6 / interval_us) if interval_us else None,
                   "achieved_per_s": m / d["wall_s"] if d["wall_s"] > 0 else None,
@@ -584,9 +585,13 @@ def config4_integrated(sv, sodium, n=48000):
     run((0, 2000), 4, 1000, 5000)  # warm-up: lane, staging and the validators' device key tables
     sv.key_cache_wait(0)
     res["paced_1k_every_5ms"] = run((2000, 32000), 4, 1000, 5000)
+    # the same bursts with the overlay posting one main-thread task per verified batch (VERDICT r5 next #7:
+    # postOnMainThread batching) instead of one per envelope
+    res["paced_1k_every_5ms_batched_post"] = run((2000, 32000), 4, 1000, 5000, batch_post=1)
     res["paced_1k_every_5ms_burst_wait_20us"] = run((2000, 32000), 4, 1000, 5000, quiet_us=20, max_linger_us=300)
     res["trickle_4_every_200us"] = run((32000, 36000), 4, 4, 200)
     res["flood"] = run((0, n), 4, 0, 0, workers=4)
+    res["flood_batched_post"] = run((0, n), 4, 0, 0, workers=4, batch_post=1)
     res["paced_1k_every_5ms_deadline_policy"] = run((36000, 46000), 4, 1000, 5000, policy=1)
     return res
 

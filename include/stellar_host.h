@@ -222,6 +222,9 @@ typedef struct svh_scp_params {
   uint32_t max_batch, max_delay_us, workers;
   uint32_t policy, linger_us, idle_in_flight;
   uint32_t quiet_us, max_linger_us; /* WhenIdle burst wait (VerifyMicroBatcher::Options; quiet 0: off) */
+  /* 1: the overlay posts one main-thread task per verified batch (submitTagged + Options::onBatch) instead of
+   * one per envelope; older callers whose struct_size ends before this field get 0 */
+  uint32_t batch_post;
 } svh_scp_params;
 typedef struct svh_scp_result {
   double verdict_p50_us, verdict_p90_us, verdict_p99_us, verdict_max_us, verdict_mean_us; /* submit -> continuation */

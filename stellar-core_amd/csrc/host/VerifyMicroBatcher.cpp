@@ -23,7 +23,8 @@ VerifyMicroBatcher::VerifyMicroBatcher(Options const& o)
       mIdleInFlight(std::max(1u, o.idleInFlight)),
       mLinger(std::min(o.linger, o.maxDelay)),
       mQuiet(o.quiet),
-      mMaxLinger(std::min(o.maxLinger, o.maxDelay)) {
+      mMaxLinger(std::min(o.maxLinger, o.maxDelay)),
+      mOnBatch(o.onBatch) {
   const unsigned w = std::max(1u, o.workers);
   mWorkers.reserve(w);
   for (unsigned i = 0; i < w; ++i) mWorkers.emplace_back([this] { run(); });
@@ -61,7 +62,7 @@ void VerifyMicroBatcher::wake() {
 }
 
 void VerifyMicroBatcher::enqueue(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg,
-                                 std::promise<bool>* done, std::function<void(bool)>* cb) {
+                                 std::promise<bool>* done, std::function<void(bool)>* cb, bool tagged, uint64_t tag) {
   // each producer thread keeps to one shard
   thread_local unsigned tShard = ~0u;
   if (tShard == ~0u) tShard = mNextShard.fetch_add(1) % kShards;
@@ -74,6 +75,8 @@ void VerifyMicroBatcher::enqueue(PublicKey const& key, ByteSlice const& sig, Byt
   r.msgLen = (uint32_t)msg.size();
   r.done = done;
   r.cb = cb;
+  r.tagged = tagged;
+  r.tag = tag;
   if (mRecordLatency) r.t0 = Clock::now();
   r.arrivalNs = nowNs();
   mNewestNs.store(r.arrivalNs, std::memory_order_relaxed);
@@ -112,6 +115,11 @@ std::future<bool> VerifyMicroBatcher::submit(PublicKey const& key, ByteSlice con
 void VerifyMicroBatcher::submit(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg,
                                 std::function<void(bool)> onVerdict) {
   enqueue(key, sig, msg, nullptr, onVerdict ? new std::function<void(bool)>(std::move(onVerdict)) : nullptr);
+}
+
+void VerifyMicroBatcher::submitTagged(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg,
+                                      uint64_t tag) {
+  enqueue(key, sig, msg, nullptr, nullptr, true, tag);
 }
 
 void VerifyMicroBatcher::post(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg) {
@@ -156,11 +164,31 @@ size_t VerifyMicroBatcher::takeFrom(size_t s, size_t want, Queue& into) {
   return want;
 }
 
+// The batch's tagged items to Options::onBatch in one call (v == nullptr: the
+// batch threw, every verdict 0).
+void VerifyMicroBatcher::deliverTagged(std::vector<Rec const*> const& recs, size_t take, std::vector<bool> const* v,
+                                       std::vector<uint64_t>& tags, std::vector<uint8_t>& verdicts) {
+  tags.clear();
+  verdicts.clear();
+  for (size_t i = 0; i < take; ++i)
+    if (recs[i]->tagged) {
+      tags.push_back(recs[i]->tag);
+      verdicts.push_back(v && (*v)[i] ? 1 : 0);
+    }
+  if (tags.empty() || !mOnBatch) return;
+  try {
+    mOnBatch(tags.data(), verdicts.data(), tags.size());
+  } catch (...) {  // (a continuation must not take the worker down)
+  }
+}
+
 void VerifyMicroBatcher::run() {
   std::vector<Queue> parts(kShards);
   std::vector<PubKeyUtils::VerifyItem> items;
   std::vector<Rec const*> recs;
   std::vector<double> lat;
+  std::vector<uint64_t> tags;  // the batch's submitTagged() items, in batch order
+  std::vector<uint8_t> tagVerdicts;
   size_t start = 0;
   std::unique_lock<std::mutex> lk(mMu);
   for (;;) {
@@ -274,6 +302,7 @@ void VerifyMicroBatcher::run() {
           delete c;
         }
       }
+      deliverTagged(recs, take, &v, tags, tagVerdicts);
     } catch (...) {  // (only a non-ed25519 key: the reference's releaseAssert)
       release();
       ok = false;
@@ -290,6 +319,7 @@ void VerifyMicroBatcher::run() {
           delete c;
         }
       }
+      deliverTagged(recs, take, nullptr, tags, tagVerdicts);
     }
     lk.lock();
     ++mStats.batches;

@@ -80,6 +80,14 @@ class VerifyMicroBatcher {
     // the timer slack.)
     std::chrono::microseconds quiet{0};
     std::chrono::microseconds maxLinger{200};
+    // Batch continuation for submitTagged() items: one call per flushed batch,
+    // onBatch(tags, verdicts, n) with the batch's tagged items in batch order,
+    // on the flush worker once their verdicts are IN THE VERIFY CACHE (after the
+    // batch's promises and per-item continuations).  What an overlay that posts
+    // one main-thread task per batch of SCP messages needs: one post per batch
+    // instead of one per envelope (Peer.cpp:977-981 posts each message).  Must
+    // not throw; a batch that throws (a non-ed25519 key) delivers 0 verdicts.
+    std::function<void(const uint64_t* tags, const uint8_t* verdicts, size_t n)> onBatch;
   };
   explicit VerifyMicroBatcher(Options const& opts);
   VerifyMicroBatcher(size_t maxBatch, std::chrono::microseconds maxDelay, unsigned workers = 2,
@@ -101,6 +109,9 @@ class VerifyMicroBatcher {
   // should be short (it delays the batch's other continuations); if the batch
   // throws (a non-ed25519 key: the reference's releaseAssert) it gets false.
   void submit(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg, std::function<void(bool)> onVerdict);
+  // Thread-safe batch-continuation form: the verdict reaches Options::onBatch
+  // with `tag`, together with the rest of its batch (no allocation per item).
+  void submitTagged(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg, uint64_t tag);
   // Blocks until every item enqueued before the call has been verified.
   void drain();
 
@@ -129,6 +140,8 @@ class VerifyMicroBatcher {
     uint64_t msgOff;           // into the arena
     std::promise<bool>* done;  // submit() only
     std::function<void(bool)>* cb;  // submit(.., onVerdict) only
+    uint64_t tag;              // submitTagged() only (tagged)
+    bool tagged;
     Clock::time_point t0;      // recordLatency only
     int64_t arrivalNs;         // deadline accounting (steady clock)
   };
@@ -143,11 +156,13 @@ class VerifyMicroBatcher {
     Queue q;
   };
   void enqueue(PublicKey const& key, ByteSlice const& sig, ByteSlice const& msg, std::promise<bool>* done,
-               std::function<void(bool)>* cb);
+               std::function<void(bool)>* cb, bool tagged = false, uint64_t tag = 0);
   void wake();
   // moves up to `want` of the oldest items of shard s into `into`; returns the count
   size_t takeFrom(size_t s, size_t want, Queue& into);
   void run();
+  void deliverTagged(std::vector<Rec const*> const& recs, size_t take, std::vector<bool> const* v,
+                     std::vector<uint64_t>& tags, std::vector<uint8_t>& verdicts);
 
   const size_t mMaxBatch;
   const std::chrono::microseconds mMaxDelay;
@@ -156,6 +171,7 @@ class VerifyMicroBatcher {
   const unsigned mIdleInFlight;
   const std::chrono::microseconds mLinger;
   const std::chrono::microseconds mQuiet, mMaxLinger;
+  const std::function<void(const uint64_t*, const uint8_t*, size_t)> mOnBatch;
   std::atomic<int64_t> mNewestNs{0};  // arrival of the newest queued item (a hint: WhenIdle's quiet period)
   unsigned mInFlight = 0;  // batches being verified (under mMu)
   Shard mShards[kShards];

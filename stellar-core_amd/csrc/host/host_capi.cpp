@@ -2,6 +2,7 @@
 // SignatureChecker / transaction-signature mirror), for bindings and tests.
 // Declared in include/stellar_host.h.  C++ exceptions never cross this
 // boundary.
+#include <cstddef>
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -471,9 +472,10 @@ int svh_mb_run_ex(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, con
 int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* msg_off,
                 const uint32_t* msg_len, size_t n, const svh_scp_params* prm, uint8_t* verdict, svh_scp_result* res) {
   try {
-    if (!prm || !res || prm->struct_size < sizeof(svh_scp_params) || n == 0 || !pk || !sig || !msg_off ||
-        !msg_len)
+    if (!prm || !res || prm->struct_size < offsetof(svh_scp_params, batch_post) || n == 0 || !pk || !sig ||
+        !msg_off || !msg_len)
       throw std::invalid_argument("svh_scp_run: bad arguments");
+    const bool batchPost = prm->struct_size >= sizeof(svh_scp_params) && prm->batch_post != 0;
     using Clk = std::chrono::steady_clock;
     const unsigned P = std::max(1u, prm->producers);
     const size_t B = prm->burst ? prm->burst : n;
@@ -505,6 +507,21 @@ int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
     mainCallUs.reserve(n);
     const Clk::time_point T0 = Clk::now() + std::chrono::milliseconds(2);
     VerifyMicroBatcher::Stats st;
+    if (batchPost)  // one main-thread post per verified batch (the envelopes in batch order)
+      o.onBatch = [&](const uint64_t* tags, const uint8_t* v, size_t m) {
+        const auto t = Clk::now();
+        for (size_t j = 0; j < m; ++j) {
+          tVer[tags[j]] = t;
+          cbVerdict[tags[j]] = v[j];
+        }
+        bool wake;
+        {
+          std::lock_guard<std::mutex> g(qm);
+          q.insert(q.end(), tags, tags + m);
+          wake = mainWaiting;
+        }
+        if (wake) qcv.notify_one();
+      };
     {
       VerifyMicroBatcher mb(o);
       // the main thread: HerderImpl::verifyEnvelope per envelope, in the order
@@ -551,6 +568,10 @@ int svh_scp_run(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const
             for (size_t i = b0 + p; i < b1; i += P) {
               std::memcpy(k.ed25519().data(), pk + 32 * i, 32);
               tSub[i] = Clk::now();
+              if (batchPost) {
+                mb.submitTagged(k, ByteSlice(sig + 64 * i, 64), ByteSlice(msg + msg_off[i], msg_len[i]), i);
+                continue;
+              }
               mb.submit(k, ByteSlice(sig + 64 * i, 64), ByteSlice(msg + msg_off[i], msg_len[i]), [&, i](bool v) {
                 tVer[i] = Clk::now();
                 cbVerdict[i] = v ? 1 : 0;

@@ -542,7 +542,7 @@ def test_micro_batcher_multiple_workers(host, engine, golden):
 class ScpParams(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint32) for k in ("struct_size", "producers", "burst", "interval_us", "max_batch",
                                                "max_delay_us", "workers", "policy", "linger_us", "idle_in_flight",
-                                               "quiet_us", "max_linger_us")]
+                                               "quiet_us", "max_linger_us", "batch_post")]
 
 
 class ScpResult(ctypes.Structure):
@@ -560,7 +560,7 @@ class ScpResult(ctypes.Structure):
 
 
 def scp_run(host, d, rows, producers, burst, interval_us, max_batch=8192, max_delay_us=2000, workers=2, policy=0,
-            linger_us=0, quiet_us=0, max_linger_us=0):
+            linger_us=0, quiet_us=0, max_linger_us=0, batch_post=0):
     """svh_scp_run (config 4 through the micro-batcher: continuation submits,
     a main thread calling verifySig per envelope) over golden rows."""
     n = len(rows)
@@ -571,7 +571,7 @@ def scp_run(host, d, rows, producers, burst, interval_us, max_batch=8192, max_de
     msg = np.ascontiguousarray(d["msg"])
     out = np.full(n, 7, np.uint8)
     p = ScpParams(ctypes.sizeof(ScpParams), producers, burst, interval_us, max_batch, max_delay_us, workers, policy,
-                  linger_us, 1, quiet_us, max_linger_us)
+                  linger_us, 1, quiet_us, max_linger_us, batch_post)
     r = ScpResult()
     vp = ctypes.c_void_p
     rc = host.svh_scp_run(vp(pk.ctypes.data), vp(sig.ctypes.data), vp(msg.ctypes.data), vp(off.ctypes.data),
@@ -618,6 +618,43 @@ def test_scp_run_bursts_many_producers(host, engine, golden):
     assert r.flushed_idle >= 1 and r.max_batch <= 8192
 
 
+def test_scp_run_batched_post(host, engine, golden):
+    """The overlay posting one main-thread task per verified batch
+    (VerifyMicroBatcher::submitTagged + Options::onBatch): the same verdicts,
+    every main-thread verifySig a hit, every envelope delivered once; and a
+    caller built against the struct without `batch_post` (struct_size ending
+    before it) still runs, per-envelope."""
+    d = golden["adversarial"]
+    seen, rows = set(), []
+    for i in range(len(d["verdict"])):
+        o, ln = int(d["msg_off"][i]), int(d["msg_len"][i])
+        k = d["pk"][i].tobytes() + d["sig"][i].tobytes() + d["msg"][o:o + ln].tobytes()
+        if k not in seen:
+            seen.add(k)
+            rows.append(i)
+    rows = np.array(rows)
+    out, r = scp_run(host, d, rows, producers=4, burst=64, interval_us=20_000, max_delay_us=500_000, batch_post=1)
+    assert (out == d["verdict"][rows]).all()
+    assert r.main_hits == len(rows) and r.main_misses == 0 and r.main_mismatches == 0
+    assert r.batches >= 1
+
+    class OldScpParams(ctypes.Structure):  # (the round-5 layout: no batch_post)
+        _fields_ = ScpParams._fields_[:-1]
+    n = 64
+    p = OldScpParams(ctypes.sizeof(OldScpParams), 2, 16, 1000, 8192, 2000, 2, 0, 0, 1, 0, 0)
+    res = ScpResult()
+    out = np.full(n, 7, np.uint8)
+    vp = ctypes.c_void_p
+    sub = rows[:n]
+    pk, sig = np.ascontiguousarray(d["pk"][sub]), np.ascontiguousarray(d["sig"][sub])
+    off, ln = np.ascontiguousarray(d["msg_off"][sub]), np.ascontiguousarray(d["msg_len"][sub])
+    rc = host.svh_scp_run(vp(pk.ctypes.data), vp(sig.ctypes.data), vp(d["msg"].ctypes.data), vp(off.ctypes.data),
+                          vp(ln.ctypes.data), ctypes.c_size_t(n), ctypes.byref(p), vp(out.ctypes.data),
+                          ctypes.byref(res))
+    assert rc == 0, host.svh_last_error_string()
+    assert (out == d["verdict"][sub]).all() and res.main_hits == n
+
+
 def test_scp_run_deadline_policy_waits(host, engine, golden):
     """The round-2 Deadline policy, for contrast: a lone envelope waits out
     maxDelay before its batch is flushed."""
@@ -645,6 +682,9 @@ def test_scp_run_quiet_period_makes_one_batch_per_burst(host, engine, golden):
     items still go at once."""
     d = golden["valid"]
     rows = np.arange(96)
+    # (a first run in a fresh process pays one-time setup inside its first
+    # batch, long enough to split that burst: run the shape once untimed)
+    scp_run(host, d, rows[:8], producers=1, burst=8, interval_us=1000, max_delay_us=400_000)
     out, r = scp_run(host, d, rows, producers=1, burst=32, interval_us=60_000, max_delay_us=400_000,
                      quiet_us=20_000, max_linger_us=300_000)
     assert (out == 1).all() and r.main_hits == len(rows)
