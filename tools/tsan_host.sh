@@ -53,6 +53,36 @@ PY
 TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$TSAN_RT \
     python3 $O/mb.py $O/libstellar_host.so "$R/tests/native/libhostcore.so" > $O/out_mb.txt 2>&1 || true
 echo "micro-batcher flood: TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out_mb.txt || true); result: $(tail -1 $O/out_mb.txt)"
+# the SCP harness (svh_scp_run: 4 producers, 2 flush workers, the main
+# thread) with per-envelope continuations and with the batch continuation
+# (submitTagged + onBatch, round 6), on the native stub engine
+cat > $O/scp.py <<'PY'
+import ctypes, sys
+import numpy as np
+host = ctypes.CDLL(sys.argv[1]); stub = ctypes.CDLL(sys.argv[2])
+host.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+host.svh_set_test_verifier(ctypes.cast(stub.hc_stub_verify, ctypes.c_void_p))
+class Prm(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint32) for k in ("struct_size", "producers", "burst", "interval_us", "max_batch",
+                "max_delay_us", "workers", "policy", "linger_us", "idle_in_flight", "quiet_us", "max_linger_us",
+                "batch_post")]
+n = 20000
+rng = np.random.default_rng(5)
+pk = rng.integers(0, 256, (n, 32), dtype=np.uint8); sig = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+msg = rng.integers(0, 256, 32 * n, dtype=np.uint8)
+off = np.arange(n, dtype=np.uint64) * 32; ln = np.full(n, 32, np.uint32); out = np.zeros(n, np.uint8)
+res = (ctypes.c_char * 4096)()
+P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+for bp in (0, 1):
+    host.svh_cache_clear()
+    p = Prm(ctypes.sizeof(Prm), 4, 500, 2000, 8192, 2000, 2, 0, 0, 1, 0, 200, bp)
+    rc = host.svh_scp_run(P(pk), P(sig), P(msg), P(off), P(ln), ctypes.c_size_t(n), ctypes.byref(p), P(out), res)
+    assert rc == 0 and out.all(), (rc, bp)
+print("ok")
+PY
+TSAN_OPTIONS="report_signal_unsafe=0 halt_on_error=0" LD_PRELOAD=$TSAN_RT \
+    python3 $O/scp.py $O/libstellar_host.so "$R/tests/native/libhostcore.so" > $O/out_scp.txt 2>&1 || true
+echo "SCP harness, per-envelope and batched posts: TSan warnings: $(grep -c 'WARNING: ThreadSanitizer' $O/out_scp.txt || true); result: $(tail -1 $O/out_scp.txt)"
 # the tx-set pre-pass (round 3): parallel marshal, SignatureBatchPrefetch::addBatch parts and
 # checkers on the pool, with the native stub engine; and the large keyed walk (threaded walk,
 # pre-drawn evictions, inline resolve) with the native keyed stub
