@@ -370,14 +370,16 @@ def test_micro_batcher_through_engine(sv, dev, golden, post):
     host.svh_cache_clear()
 
 
-@pytest.mark.parametrize("burst,interval_us,linger_us,quiet_us",
-                         [(500, 2000, 0, 10), (4, 100, 0, 10), (0, 0, 0, 10), (500, 2000, 50, 0), (500, 2000, 0, 0)])
-def test_scp_integrated_path(sv, dev, golden, burst, interval_us, linger_us, quiet_us):
+@pytest.mark.parametrize("burst,interval_us,linger_us,quiet_us,batch_post",
+                         [(500, 2000, 0, 10, 0), (4, 100, 0, 10, 0), (0, 0, 0, 10, 0), (500, 2000, 50, 0, 0),
+                          (500, 2000, 0, 0, 0), (500, 2000, 0, 0, 1), (0, 0, 0, 0, 1)])
+def test_scp_integrated_path(sv, dev, golden, burst, interval_us, linger_us, quiet_us, batch_post):
     """Config 4 through the integration path on the GPU (svh_scp_run): overlay
     producers -> VerifyMicroBatcher (WhenIdle) -> keyed verifySigBatch (GPU
     BLAKE2b keys, mapped keys / verdicts on the latency lane) -> continuation
     -> main-thread verifySig.  Distinct adversarial + 0..512 B rows: every
-    verdict equals libsodium's, every main-thread call is a cache hit."""
+    verdict equals libsodium's, every main-thread call is a cache hit; with
+    one continuation per envelope and (batch_post) one per verified batch."""
     from test_host_mirror import scp_run
     host = _host(sv)
     host.svh_scp_run.restype = ctypes.c_int
@@ -398,7 +400,7 @@ def test_scp_integrated_path(sv, dev, golden, burst, interval_us, linger_us, qui
     host.svh_cache_clear()
     _stats(host)
     out, r = scp_run(host, d, rows, producers=4, burst=burst, interval_us=interval_us, linger_us=linger_us,
-                     quiet_us=quiet_us, max_linger_us=200)
+                     quiet_us=quiet_us, max_linger_us=200, batch_post=batch_post)
     assert np.array_equal(out, d["verdict"][rows])
     assert r.main_hits == len(rows) and r.main_misses == 0 and r.main_mismatches == 0
     assert r.fallbacks == 0 and r.gpu_batches >= 1
