@@ -129,13 +129,18 @@ void svh_set_keyed_threshold(size_t min_items);
 /* use_prefetch: 0 none; 1 one batch pre-pass into a side table (pairs
  * enumerated in parallel, each checker finds its tx's pairs by position); 2
  * the same through verifySigBatch (also seeds the verify cache); 3 as 1 with
- * the checkers looking their pairs up in the table only */
+ * the checkers looking their pairs up in the table only; 4 as 1 in two halves,
+ * pipelined: the engine verifies half 0 while half 1 is enumerated and half 1
+ * while half 0's checkers run (sets of at least 1024 transactions; smaller
+ * ones run as 1).  Outcomes are the same in every mode. */
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs);
 /* Wall-clock phases (ms) of the calling thread's last svh_check_txset:
  * [0] C structs -> the mirror's objects, [1] pair enumeration (prefetch add),
  * [2] the engine pre-pass (prefetch run: one GPU batch + side table),
- * [3] the checkers.  [1] and [2] are 0 without the pre-pass. */
+ * [3] the checkers.  [1] and [2] are 0 without the pre-pass.  Pipelined (use_prefetch 4): [1] half 0's
+ * enumeration, [2] the overlapped middle (engine on half 0 beside half 1's enumeration, then engine on
+ * half 1 beside half 0's checkers), [3] half 1's checkers. */
 void svh_txset_last_phases(double out[4]);
 
 /* ---- transaction-level checks (a13) ---- */

@@ -82,19 +82,25 @@ void SignatureBatchPrefetch::Storage::clear() {
   txBegin.clear();
 }
 
-SignatureBatchPrefetch::Storage& SignatureBatchPrefetch::spare() {
-  thread_local Storage s;
+// A few spares per thread: a call that holds several prefetches at once (the
+// pipelined tx-set pre-pass holds two) reuses the storage of each.
+std::vector<SignatureBatchPrefetch::Storage>& SignatureBatchPrefetch::spares() {
+  thread_local std::vector<Storage> s;
   return s;
 }
 
 SignatureBatchPrefetch::SignatureBatchPrefetch() {
-  std::swap(st_, spare());  // (the spare is left empty; a nested prefetch allocates afresh)
+  auto& sp = spares();
+  if (!sp.empty()) {
+    std::swap(st_, sp.back());
+    sp.pop_back();
+  }
   st_.clear();
 }
 
 SignatureBatchPrefetch::~SignatureBatchPrefetch() {
-  Storage& sp = spare();
-  if (sp.pk.capacity() < st_.pk.capacity()) std::swap(sp, st_);
+  auto& sp = spares();
+  if (sp.size() < kSpares) sp.push_back(std::move(st_));
 }
 uint64_t SignatureBatchPrefetch::hashOf(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, size_t len) {
   // signatures and keys are uniformly distributed bytes: a few words of each

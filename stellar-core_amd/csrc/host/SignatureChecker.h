@@ -71,8 +71,8 @@ bool verifyEd25519SignedPayload(DecoratedSignature const& sig, SignerKey const& 
 // Verdicts computed ahead of the checkers.
 class SignatureBatchPrefetch {
  public:
-  // Storage is taken from (and on destruction returned to) a per-thread
-  // spare, so a node building one prefetch per ledger reuses mapped pages
+  // Storage is taken from (and on destruction returned to) per-thread
+  // spares, so a node building one prefetch per ledger reuses mapped pages
   // instead of faulting in fresh ones every time (measured: page faults of
   // freshly grown buffers were most of the cost of add() on a 30k-pair set).
   SignatureBatchPrefetch();
@@ -147,7 +147,8 @@ class SignatureBatchPrefetch {
   };
   static void enumerate(Storage& st, Hash const& contentsHash, std::vector<DecoratedSignature> const& signatures,
                         std::vector<Signer> const& signers);
-  static Storage& spare();
+  static std::vector<Storage>& spares();
+  static constexpr size_t kSpares = 4;
   Storage st_;
   RawVec<uint8_t>& pk_ = st_.pk;
   RawVec<uint8_t>& sig_ = st_.sig;

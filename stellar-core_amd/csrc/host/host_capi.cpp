@@ -3,6 +3,7 @@
 // Declared in include/stellar_host.h.  C++ exceptions never cross this
 // boundary.
 #include <cstddef>
+#include <future>
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -240,6 +241,10 @@ void svh_set_test_keyed_verifier(svh_keyed_verify_fn fn) { PubKeyUtils::setKeyed
 void svh_set_keyed_threshold(size_t min_items) { PubKeyUtils::setKeyedBatchThreshold(min_items); }
 void svh_set_cpu_threshold(size_t max_misses) { PubKeyUtils::setCpuBatchThreshold(max_misses); }
 
+// Below this many transactions the pipelined pre-pass (use_prefetch 4) runs
+// as one batch: its halves would leave the engine's lane and the pool idle.
+constexpr size_t kPipelineMinTxs = 1024;
+
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs) {
   try {
@@ -286,6 +291,59 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
       for (uint32_t k = 0; k < txs[t].nsigners; ++k) signerInto(sgn[t][k], signers[txs[t].signer_off + k]);
     };
     double ph[4] = {0, 0, 0, 0};
+    // use_prefetch 4: the side-table pre-pass in two halves, pipelined -- the
+    // engine verifies half 0's pairs while half 1 is enumerated, and half 1's
+    // while half 0's checkers run (each half its own prefetch, so neither's
+    // storage moves under the other's engine call).  Same pairs, verdicts and
+    // checker outcomes as mode 1; smaller sets run as mode 1.
+    if (use_prefetch == 4 && ntx >= kPipelineMinTxs) {
+      const size_t half = ntx / 2, lo[2] = {0, half}, hi[2] = {half, ntx};
+      SignatureBatchPrefetch pres[2];
+      std::vector<SignatureBatchPrefetch::TxRef> refs(ntx);
+      for (size_t t = 0; t < ntx; ++t) refs[t] = {&hashes[t], &dsigs[t], &sgn[t]};
+      ph[0] = pc.lap("txset: marshal (alloc)");
+      auto enumerate = [&](int h) {
+        std::vector<SignatureBatchPrefetch::TxRef> part(refs.begin() + (ptrdiff_t)lo[h], refs.begin() + (ptrdiff_t)hi[h]);
+        pres[h].addBatch(part, [&, h](size_t k) { marshal(lo[h] + k); });
+      };
+      auto checkers = [&](int h) {
+        parallelOrThrow(hi[h] - lo[h], 128, [&, h](size_t a, size_t b) {
+          for (size_t t = lo[h] + a; t < lo[h] + b; ++t) {
+            SignatureChecker c(txs[t].protocol, hashes[t], dsigs[t], &pres[h], t - lo[h]);
+            ok[t] = c.checkSignature(sgn[t], txs[t].needed_weight) ? 1 : 0;
+            all_used[t] = c.checkAllSignaturesUsed() ? 1 : 0;
+          }
+        });
+      };
+      // the engine calls run on a thread of their own (std::async); an
+      // exception in either is rethrown by its get()
+      enumerate(0);
+      ph[1] = pc.lap("txset: half 0 marshal + prefetch add");
+      auto e0 = std::async(std::launch::async, [&] { pres[0].run(false); });
+      std::exception_ptr failed;
+      try {
+        enumerate(1);
+      } catch (...) {
+        failed = std::current_exception();
+      }
+      e0.get();
+      if (failed) std::rethrow_exception(failed);
+      auto e1 = std::async(std::launch::async, [&] { pres[1].run(false); });
+      try {
+        checkers(0);
+      } catch (...) {
+        failed = std::current_exception();
+      }
+      e1.get();
+      if (failed) std::rethrow_exception(failed);
+      ph[2] = pc.lap("txset: engine 0 | half 1 add, engine 1 | half 0 checkers");
+      checkers(1);
+      ph[3] = pc.lap("txset: half 1 checkers");
+      if (prefetched_pairs) *prefetched_pairs = pres[0].pairs() + pres[1].pairs();
+      std::memcpy(t_txset_phases, ph, sizeof ph);
+      return SVH_OK;
+    }
+    if (use_prefetch == 4) use_prefetch = 1;
     SignatureBatchPrefetch pre;
     if (use_prefetch) {
       // with the pre-pass each tx is marshalled by the pool thread that

@@ -416,6 +416,18 @@ def test_txset_prefetch_parallel_batch_matches_replay(host, engine, oracle):
     ok3, used3, pairs3 = _check(host, txs, 3)
     assert engine.calls - calls_before == 1 and pairs3 == pairs
     assert (ok3 == want_ok).all() and (used3 == want_used).all()
+    # pipelined in two halves (use_prefetch 4): two engine batches, the same pairs and outcomes
+    host.svh_cache_clear()
+    calls_before = engine.calls
+    ok4, used4, pairs4 = _check(host, txs, 4)
+    assert engine.calls - calls_before == 2 and pairs4 == pairs
+    assert (ok4 == want_ok).all() and (used4 == want_used).all()
+    # (a set below the pipeline's minimum runs as one batch)
+    small = txs[:200]
+    calls_before = engine.calls
+    ok5, used5, _ = _check(host, small, 4)
+    assert engine.calls - calls_before == 1
+    assert (ok5 == want_ok[:200]).all() and (used5 == want_used[:200]).all()
 
 
 def test_txset_bad_signer_in_parallel_marshal_is_an_error(host, engine, oracle):
@@ -423,12 +435,12 @@ def test_txset_bad_signer_in_parallel_marshal_is_an_error(host, engine, oracle):
     back as SVH_ERR_INVALID_ARG with its message (never an exception escaping a
     pool thread)."""
     sign = _oracle_sign_fn(oracle)
-    txs = tg.generate(900, sign, seed=5)
+    txs = tg.generate(1100, sign, seed=5)  # (>= 1024: the pipelined mode 4 splits it; the bad signer is in half 1)
     T, S, G = tg.to_ctypes(txs)
     G[len(G) - 3].type = 7  # no such signer type
     ok = np.zeros(len(txs), np.uint8)
     used = np.zeros(len(txs), np.uint8)
-    for prefetch in (1, 0):
+    for prefetch in (1, 0, 4):
         rc = host.svh_check_txset(T, ctypes.c_size_t(len(txs)), S, G, prefetch, ok.ctypes.data_as(ctypes.c_void_p),
                                   used.ctypes.data_as(ctypes.c_void_p), None)
         assert rc != 0
