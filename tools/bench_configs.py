@@ -300,25 +300,39 @@ def config3(env, n_tx=5000, sets=5):
     gen_s = (time.perf_counter() - t0) / (sets + 1)
     txs, cts = built[0]
     nsig = sum(len(t["sigs"]) for t in txs)
-    ok_g, used_g, dt_first, pairs = run(cts, 1)
+    # the headline runs the pipelined pre-pass (svh_check_txset use_prefetch 4: two halves, the engine on one
+    # beside the host work of the other); the one-batch pre-pass (use_prefetch 1) is timed beside it
+    ok_g, used_g, dt_first, pairs = run(cts, 4)
+    run(cts, 1)
     del phases[:]
-    outs = [run(b[1], 1) for b in built[1:]]  # each distinct set once
+    outs = [run(b[1], 4) for b in built[1:]]  # each distinct set once
     dts = [o[2] for o in outs]
     ph = np.array(phases)  # the distinct sets' phases, in ms
+    outs1 = [run(b[1], 1) for b in built[1:]]
+    dts1 = [o[2] for o in outs1]
+    ph1 = np.array(phases[len(outs):])
+    same_as_one_batch = all((a[0] == b[0]).all() and (a[1] == b[1]).all() for a, b in zip(outs, outs1))
     phase_split = {k: float(np.median(ph[:, j])) for j, k in enumerate(
-        ("marshal_ms", "pair_enumeration_ms", "engine_prepass_ms", "checkers_ms"))}
+        ("marshal_ms", "half0_pair_enumeration_ms", "overlapped_engine_and_host_ms", "half1_checkers_ms"))}
     phase_split["per_set"] = [[round(float(x), 3) for x in row] for row in ph]
-    phase_split["what"] = ("svh_txset_last_phases medians over the distinct sets: marshal = the mirror objects' "
-                           "allocation (the C structs are marshalled per tx inside the pair-enumeration pass, "
-                           "SignatureBatchPrefetch::addBatch with its prepare hook), run() (one GPU batch + side "
-                           "table), the checkers on the host pool")
-    dt_rep = min(run(cts, 1)[2] for _ in range(3))  # the first set again (warm per-key state): not the headline
+    phase_split["what"] = ("svh_txset_last_phases medians over the distinct sets, pipelined pre-pass: the mirror "
+                           "objects' allocation; half 0's marshal + pair enumeration (SignatureBatchPrefetch::"
+                           "addBatch); engine on half 0 beside half 1's enumeration, then engine on half 1 beside "
+                           "half 0's checkers; half 1's checkers")
+    phase_split_one_batch = {k: float(np.median(ph1[:, j])) for j, k in enumerate(
+        ("marshal_ms", "pair_enumeration_ms", "engine_prepass_ms", "checkers_ms"))}
+    dt_rep = min(run(cts, 4)[2] for _ in range(3))  # the first set again (warm per-key state): not the headline
     out = {"txs": n_tx, "decorated_signatures": nsig, "prefetched_pairs": pairs, "generate_s": gen_s,
            "distinct_sets": sets,
            "gpu_prepass_checker_s": float(np.median(dts)), "gpu_prepass_checker_max_s": float(max(dts)),
            "gpu_prepass_checker_first_call_s": dt_first, "gpu_prepass_same_set_repeat_min_s": dt_rep,
            "gpu_prepass_txs_per_s": n_tx / float(np.median(dts)),
+           "prepass_mode": "pipelined (svh_check_txset use_prefetch 4)",
            "phase_split": phase_split,
+           "one_batch_prepass": {"median_s": float(np.median(dts1)), "max_s": float(max(dts1)),
+                                 "phase_split": phase_split_one_batch,
+                                 "outcomes_equal_pipelined": bool(same_as_one_batch),
+                                 "what": "the same sets through the one-batch pre-pass (use_prefetch 1)"},
            "timing": "median / max over %d distinct sets, each checked once after a first (warm-up) set; "
                      "first_call = the process's first set" % sets}
     if env.have_sodium:
