@@ -103,7 +103,7 @@ txs = tg.generate(2000, sign, seed=7)
 T, S, G = tg.to_ctypes(txs)
 host.svh_set_test_verifier(ctypes.cast(stub.hc_stub_verify, ctypes.c_void_p))
 ok = np.zeros(len(txs), np.uint8); used = np.zeros(len(txs), np.uint8)
-for pf in (1, 3, 1):
+for pf in (1, 3, 4, 1):
     rc = host.svh_check_txset(T, ctypes.c_size_t(len(txs)), S, G, pf, ok.ctypes.data_as(ctypes.c_void_p),
                               used.ctypes.data_as(ctypes.c_void_p), None)
     assert rc == 0, rc
