@@ -1057,7 +1057,8 @@ def test_gpu_config3_full_5000_tx(host, sv, oracle):
     """BASELINE config 3 at full size: a 5000-tx set with 1-20 ED25519 signers
     per tx (plus PRE_AUTH_TX / HASH_X / signed-payload signers, colliding-hint
     wrong keys, unused and short signatures), checked after ONE GPU pre-pass
-    (side table, and seeding the cache); outcomes == the independent Python
+    (side table, and seeding the cache) and after the pipelined two-half
+    pre-pass; outcomes == the independent Python
     replay of SignatureChecker.cpp:30-158 with oracle verdicts."""
     if sv.device_count() < 1:
         pytest.skip("no GPU")
@@ -1085,7 +1086,7 @@ def test_gpu_config3_full_5000_tx(host, sv, oracle):
 
     want_ok, want_used = tg.replay(txs, verify)
     host.svh_set_test_verifier(None)
-    for mode in (1, 2):
+    for mode in (1, 2, 4):  # (4: the pipelined pre-pass, two engine batches)
         host.svh_cache_clear()
         ok, used, pairs = _check(host, txs, mode)
         assert (ok == want_ok).all() and (used == want_used).all(), mode
