@@ -2,11 +2,10 @@
 // SignatureChecker / transaction-signature mirror), for bindings and tests.
 // Declared in include/stellar_host.h.  C++ exceptions never cross this
 // boundary.
-#include <cstddef>
-#include <future>
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -245,6 +244,64 @@ void svh_set_cpu_threshold(size_t max_misses) { PubKeyUtils::setCpuBatchThreshol
 // as one batch: its halves would leave the engine's lane and the pool idle.
 constexpr size_t kPipelineMinTxs = 1024;
 
+// One helper thread per calling thread, kept for that thread's life: the
+// pipelined pre-pass runs its engine calls on it (a thread created per call
+// cost tens of microseconds on a loaded host).  start() hands it one task;
+// wait() returns when it is done and rethrows what it threw.
+class CallHelper {
+ public:
+  CallHelper() : thread_([this] { loop(); }) {}
+  ~CallHelper() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    thread_.join();
+  }
+  void start(std::function<void()> f) {
+    std::lock_guard<std::mutex> g(mu_);
+    task_ = std::move(f);
+    err_ = nullptr;
+    pending_ = true;
+    done_ = false;
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return done_; });
+    if (err_) std::rethrow_exception(err_);
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || pending_; });
+      if (stop_) return;
+      std::function<void()> f = std::move(task_);
+      pending_ = false;
+      lk.unlock();
+      std::exception_ptr e;
+      try {
+        f();
+      } catch (...) {
+        e = std::current_exception();
+      }
+      lk.lock();
+      err_ = e;
+      done_ = true;
+      cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::function<void()> task_;
+  std::exception_ptr err_;
+  bool pending_ = false, done_ = true, stop_ = false;
+  std::thread thread_;  // (last: started once the state above exists)
+};
+
 int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs, const svh_signer* signers,
                     int use_prefetch, uint8_t* ok, uint8_t* all_used, uint64_t* prefetched_pairs) {
   try {
@@ -315,26 +372,27 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
           }
         });
       };
-      // the engine calls run on a thread of their own (std::async); an
-      // exception in either is rethrown by its get()
+      // the engine calls run on this thread's helper; an exception in either
+      // is rethrown by wait(), after this thread's own part has finished
+      thread_local CallHelper helper;
       enumerate(0);
       ph[1] = pc.lap("txset: half 0 marshal + prefetch add");
-      auto e0 = std::async(std::launch::async, [&] { pres[0].run(false); });
+      helper.start([&] { pres[0].run(false); });
       std::exception_ptr failed;
       try {
         enumerate(1);
       } catch (...) {
         failed = std::current_exception();
       }
-      e0.get();
+      helper.wait();
       if (failed) std::rethrow_exception(failed);
-      auto e1 = std::async(std::launch::async, [&] { pres[1].run(false); });
+      helper.start([&] { pres[1].run(false); });
       try {
         checkers(0);
       } catch (...) {
         failed = std::current_exception();
       }
-      e1.get();
+      helper.wait();
       if (failed) std::rethrow_exception(failed);
       ph[2] = pc.lap("txset: engine 0 | half 1 add, engine 1 | half 0 checkers");
       checkers(1);
