@@ -10,6 +10,11 @@ Threads run for SECONDS, each checking every verdict it gets:
             (checked against hashlib)
   device    sv_ed25519_verify_device on its own torch stream, with the bitmap
   cpu       the engine's CPU path on small batches
+  txset     the C++ mirror's tx-set check with the pipelined pre-pass
+            (svh_check_txset use_prefetch 4), outcomes against the same
+            set's one-batch outcomes taken before the soak
+  scp       the SCP harness (svh_scp_run: micro-batcher, batched main-thread
+            post, main-thread verifySig), verdicts and cache hits
 Rows come from the engine's GPU signer (valid) with one random bit flipped in
 R, S, A or the message on a random third of them (rejected), so the expected
 verdicts are known without libsodium.  Prints one JSON line: per-thread call
@@ -183,7 +188,82 @@ def main():
                                       np.full(n, 32, np.uint32), threads=1)
             record("cpu", 1, n, int((got != want).sum()))
 
-    workers = [bulk, bulk, lane, lane, keyed, device, cpu]
+    # the host-integration workers (libstellar_host): a 3000-tx set and SCP-shaped bursts
+    import ctypes
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import txset_gen as tg
+
+    host = ctypes.CDLL(sv.HOSTLIB_PATH)
+    host.svh_last_error_string.restype = ctypes.c_char_p
+    host.svh_set_test_verifier.argtypes = [ctypes.c_void_p]
+    host.svh_set_test_verifier(None)
+    def sign_fn(reqs):  # the engine's RFC 8032 signer over the generator's (seed, message) requests
+        n = len(reqs)
+        ts = torch.from_numpy(np.frombuffer(b"".join(r[0] for r in reqs), np.uint8).reshape(n, 32).copy()).to(dev)
+        tmm = torch.from_numpy(np.frombuffer(b"".join(r[1] for r in reqs), np.uint8).reshape(n, 32).copy()).to(dev)
+        tp = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        tsg = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+        sv.sign_device(0, ts.data_ptr(), tmm.data_ptr(), n, tp.data_ptr(), tsg.data_ptr(),
+                       torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        a, b = tp.cpu().numpy(), tsg.cpu().numpy()
+        return [(a[i].tobytes(), b[i].tobytes()) for i in range(n)]
+
+    # (outcomes are compared with the same set's one-batch outcomes, taken before the soak)
+    txs = tg.generate(3000, sign_fn, seed=31)
+    T, S, G = tg.to_ctypes(txs)
+    nt = len(txs)
+
+    def check_txset(mode):
+        ok = np.zeros(nt, np.uint8)
+        used = np.zeros(nt, np.uint8)
+        rc = host.svh_check_txset(T, ctypes.c_size_t(nt), S, G, mode, ok.ctypes.data_as(ctypes.c_void_p),
+                                  used.ctypes.data_as(ctypes.c_void_p), None)
+        if rc != 0:
+            raise RuntimeError(host.svh_last_error_string())
+        return ok, used
+
+    want_ok, want_used = check_txset(1)
+
+    def txset(seed):
+        while time.time() < stop:
+            try:
+                ok, used = check_txset(4)
+                record("txset", 1, nt, int((ok != want_ok).sum() + (used != want_used).sum()))
+            except Exception as e:
+                record("txset", 1, 0, 0, repr(e))
+
+    class Prm(ctypes.Structure):
+        _fields_ = [(k, ctypes.c_uint32) for k in ("struct_size", "producers", "burst", "interval_us", "max_batch",
+                    "max_delay_us", "workers", "policy", "linger_us", "idle_in_flight", "quiet_us",
+                    "max_linger_us", "batch_post")]
+
+    def scp(seed):
+        rng = np.random.default_rng(seed)
+        res = (ctypes.c_char * 4096)()
+        while time.time() < stop:
+            n = 2000
+            rows = rng.integers(0, 6400, n)
+            p, s, m, want = corrupt(rng, vpk[rows], vsig[rows], vmsg[rows], keys_too=False)
+            # distinct envelopes (a duplicate in flight in two batches reads as a miss, as for concurrent calls)
+            _, first = np.unique(np.concatenate([p, s, m], axis=1), axis=0, return_index=True)
+            first = np.sort(first)
+            p, s, m, want = (np.ascontiguousarray(x[first]) for x in (p, s, m, want))
+            n = len(first)
+            off = np.arange(n, dtype=np.uint64) * 32
+            ln = np.full(n, 32, np.uint32)
+            out = np.full(n, 7, np.uint8)
+            prm = Prm(ctypes.sizeof(Prm), 2, 500, 2000, 8192, 2000, 2, 0, 0, 1, 0, 200, 1)
+            host.svh_cache_clear()
+            P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+            rc = host.svh_scp_run(P(p), P(s), P(m.reshape(-1)), P(off), P(ln), ctypes.c_size_t(n), ctypes.byref(prm),
+                                  P(out), res)
+            if rc != 0:
+                record("scp", 1, 0, 0, host.svh_last_error_string().decode())
+                continue
+            record("scp", 1, n, int((out != want).sum()))
+
+    workers = [bulk, bulk, lane, lane, keyed, device, cpu, txset, scp]
     th = [threading.Thread(target=f, args=(100 + k,)) for k, f in enumerate(workers)]
     t0 = time.time()
     last = t0
