@@ -360,7 +360,8 @@ int svh_check_txset(const svh_tx* txs, size_t ntx, const svh_decorated_sig* sigs
       for (size_t t = 0; t < ntx; ++t) refs[t] = {&hashes[t], &dsigs[t], &sgn[t]};
       ph[0] = pc.lap("txset: marshal (alloc)");
       auto enumerate = [&](int h) {
-        std::vector<SignatureBatchPrefetch::TxRef> part(refs.begin() + (ptrdiff_t)lo[h], refs.begin() + (ptrdiff_t)hi[h]);
+        std::vector<SignatureBatchPrefetch::TxRef> part(refs.begin() + (ptrdiff_t)lo[h],
+                                                        refs.begin() + (ptrdiff_t)hi[h]);
         pres[h].addBatch(part, [&, h](size_t k) { marshal(lo[h] + k); });
       };
       auto checkers = [&](int h) {
